@@ -1,0 +1,148 @@
+"""Throughput benchmark: the flagship training step on N GPUs of one node.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model cnn|linear]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): images/sec for the whole node, MNIST CNN (SURVEY.md §7.1:
+conv 1->32 3x3 + ReLU, conv 32->64 3x3 + ReLU, maxpool 2, fc 9216->128 + ReLU,
+fc 128->10, log-softmax/NLL) trained with DDP (bucketed RCCL all-reduce over
+xGMI) and SGD-momentum, bf16 compute / fp32 master weights, on synthetic
+1x28x28 data of MNIST size (60k) with random-init weights.  Per-GPU batch is
+fixed (weak scaling): 256 images per rank by default, the reference's per-GPU
+batch at world_size 1 (its --batch-size 256 is split over the GPUs).
+
+A timed step is the complete training step: batch gather + normalise,
+forward, loss, backward, gradient all-reduce, optimizer update (incl. the
+epoch-boundary reshuffles that fall inside the window).  W untimed warmup
+steps, then exactly K steps bracketed by a barrier + device synchronize on
+both sides; the slowest rank's time is reported.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--model", choices=["cnn", "linear"], default="cnn")
+    ap.add_argument("--batch-per-rank", type=int, default=256)
+    ap.add_argument("--optimizer", choices=["sgd", "adam"], default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--no-graphs", dest="graphs", action="store_false")
+    ap.add_argument("--train-size", type=int, default=60000)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != a.gpus:
+        if ws == 1 and a.gpus > 1:
+            print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} procs",
+                  file=sys.stderr)
+            sys.exit(2)
+    from pytorch_distributed_mnist_amd import parallel
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.models.reference import MODULES
+    from pytorch_distributed_mnist_amd.models.specs import get_spec
+    from pytorch_distributed_mnist_amd.optim.flat import build_optimizer
+    from pytorch_distributed_mnist_amd.runtime.arena import FlatArena
+    from pytorch_distributed_mnist_amd.runtime.program import TrainProgram
+    from types import SimpleNamespace
+
+    device = parallel.pick_device(local_rank, "cuda")
+    ctx = parallel.init_distributed("nccl", "env://" if ws > 1 else None, ws, rank, local_rank,
+                                    device, init_pg=ws > 1)
+    comm = parallel.make_comm(ctx)
+    model = a.model
+    dtype = "bf16" if model == "cnn" else "fp32"
+    optname = a.optimizer or ("sgd" if model == "cnn" else "adam")
+    lr = a.lr if a.lr is not None else (0.01 if optname == "sgd" else 1e-3)
+
+    torch.manual_seed(1234 + rank)
+    spec = get_spec(model)
+    arena = FlatArena(spec, device)
+    arena.load_module(MODULES[model]())
+    comm.broadcast_(arena.params, 0)
+    opt = build_optimizer(optname, arena, SimpleNamespace(lr=lr, momentum=0.9, weight_decay=1e-4))
+    reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds())
+    train = synthetic_split(a.train_size, True)
+    test = synthetic_split(1024, False)
+    B = a.batch_per_rank
+    prog = TrainProgram(model, dtype, arena, opt, reducer, train, test, B, use_graphs=a.graphs)
+    n = len(train)
+
+    state = {"epoch": 0, "step": 0}
+
+    def next_epoch():
+        prog.set_train_indices(distributed_indices(n, ws, rank, state["epoch"]))
+        prog.gpu.begin_epoch()
+        state["epoch"] += 1
+        state["step"] = 0
+
+    def run(k):
+        full = prog.steps_per_epoch - (1 if (n // ws) % B else 0)   # full-batch steps
+        for _ in range(k):
+            if state["step"] >= full:
+                next_epoch()
+            prog.gpu.train_step(B)
+            state["step"] += 1
+
+    opt.sync_hyperparams()
+    next_epoch()
+    run(a.warmup)
+
+    def barrier():
+        if ws > 1:
+            torch.distributed.barrier()
+
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(a.steps)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if not torch.isfinite(arena.params).all():
+        raise RuntimeError("non-finite parameters after the benchmark")
+    ms = elapsed / a.steps * 1e3
+    global_batch = B * ws
+    value = a.steps * global_batch / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node) MNIST CNN DDP at 1/2/4/8 MI355X"
+            if model == "cnn" else "images/sec (whole node) MNIST Linear DDP",
+            "value": round(value, 1), "unit": "images/sec", "n_gpus": ws, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+            "data": "synthetic (60k x 1x28x28 uint8, MNIST-shaped), random-init weights",
+            "config": {"model": "mnist_cnn" if model == "cnn" else "mnist_linear",
+                       "global_batch": global_batch, "batch_per_rank": B, "seq_len": None,
+                       "parallelism": f"dp{ws}", "optimizer": optname,
+                       "graphs": bool(prog.gpu.use_graphs)},
+        }), flush=True)
+    comm.close()
+    parallel.shutdown()
+
+
+if __name__ == "__main__":
+    main()

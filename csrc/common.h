@@ -1,0 +1,54 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+// Wave64 everywhere: lane = threadIdx.x & 63, block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define PDM_WAVE 64
+
+// torchvision ToTensor() + Normalize((0.1307,), (0.3081,)) in fp32, same op order
+// (x/255, then (x-mean)/std; HIP's default fp32 division is correctly rounded).
+__device__ __forceinline__ float pdm_normalize(uint32_t v) {
+  return ((float)v / 255.0f - 0.1307f) / 0.3081f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Sum within aligned groups of `width` lanes (width a power of two <= 64).
+template <int WIDTH>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ bf16 to_bf16(float f) { return (bf16)f; }
+__device__ __forceinline__ float from_bf16(bf16 h) { return (float)h; }
+
+// Bookkeeping done by exactly one thread of a kernel that no other kernel of the
+// same step reads concurrently (see runtime/gpu_step.py: the "middle" kernel
+// advances the data-step and optimizer-step counters).
+__device__ __forceinline__ void pdm_bump_counters(int64_t* c0, int64_t* c1) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (c0) *c0 += 1;
+    if (c1) *c1 += 1;
+  }
+}

@@ -1,0 +1,70 @@
+"""Per-rank sample order, bit-identical to ``torch.utils.data.DistributedSampler``.
+
+The reference wraps the training set in ``data.DistributedSampler(dataset)``
+(reference ``multi_proc_single_gpu.py:142-144``) with the defaults shuffle=True,
+seed=0, drop_last=False, and calls ``set_epoch(epoch)`` every epoch
+(``multi_proc_single_gpu.py:159-161, 231``).  The test loader is sequential and
+unsharded (``multi_proc_single_gpu.py:146-149``).
+
+Instead of a Python iterator feeding DataLoader workers, we materialise the whole
+epoch's index vector once (one ``randperm`` on the host, ~1 ms for 60k) and upload
+it to the device as int32; the step kernels then gather their batch straight from
+the device-resident uint8 dataset.  The vector is computed with tensor ops (no
+Python lists) but reproduces the sampler's padding/striding rules exactly, which
+tests/test_sampler.py checks against torch's own class.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def num_samples_per_rank(n: int, world_size: int, drop_last: bool = False) -> int:
+    if drop_last and n % world_size != 0:
+        return math.ceil((n - world_size) / world_size)
+    return math.ceil(n / world_size)
+
+
+def distributed_indices(n: int, world_size: int, rank: int, epoch: int, *,
+                        seed: int = 0, shuffle: bool = True,
+                        drop_last: bool = False) -> torch.Tensor:
+    """Indices rank ``rank`` visits in ``epoch`` (int64 CPU tensor)."""
+    if not 0 <= rank < world_size:
+        raise ValueError(f"rank {rank} out of range for world_size {world_size}")
+    if shuffle:
+        g = torch.Generator()
+        g.manual_seed(seed + epoch)
+        order = torch.randperm(n, generator=g)
+    else:
+        order = torch.arange(n)
+    per_rank = num_samples_per_rank(n, world_size, drop_last)
+    total = per_rank * world_size
+    if not drop_last:
+        pad = total - n
+        if pad > 0:
+            if pad <= n:
+                order = torch.cat([order, order[:pad]])
+            else:
+                reps = math.ceil(pad / n)
+                order = torch.cat([order, order.repeat(reps)[:pad]])
+    else:
+        order = order[:total]
+    return order[rank:total:world_size].contiguous()
+
+
+def sequential_indices(n: int) -> torch.Tensor:
+    return torch.arange(n, dtype=torch.int64)
+
+
+def batch_bounds(num: int, batch_size: int, drop_last: bool = False):
+    """[(start, size)] of the batches a DataLoader would produce over ``num`` samples."""
+    out = []
+    start = 0
+    while start < num:
+        size = min(batch_size, num - start)
+        if drop_last and size < batch_size:
+            break
+        out.append((start, size))
+        start += size
+    return out

@@ -1,0 +1,116 @@
+"""Data-plane communicators.
+
+``RcclComm`` is the MI355X path: a C++ wrapper around an RCCL communicator
+(``ncclCommInitRank``) that owns its own HIP stream (``csrc/runtime/comm.cpp``).
+The ``ncclUniqueId`` is exchanged through the rendezvous TCP store of the
+default process group, honouring ``--init-method tcp://host:port`` /
+``env://``.  Collectives are enqueued on the comm stream
+behind an event recorded on the caller's stream, and the caller's stream is
+made to wait for completion, so they compose with hipGraph capture.
+
+``TorchComm`` routes through ``torch.distributed`` (gloo) and is what the CPU
+path and ``--backend gloo`` use.  ``LocalComm`` is world_size 1 without any
+process group (bench at N=1): every collective is the identity.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+from .dist import default_store, distributed_is_initialized
+
+_uid_counter = itertools.count()
+
+
+class Communicator:
+    rank: int = 0
+    world_size: int = 1
+    native: bool = False
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class LocalComm(Communicator):
+    def __init__(self):
+        self.rank, self.world_size = 0, 1
+
+    def all_reduce_(self, t):
+        return t
+
+    def broadcast_(self, t, src=0):
+        return t
+
+
+class TorchComm(Communicator):
+    def __init__(self):
+        if not distributed_is_initialized():
+            raise RuntimeError("TorchComm needs an initialised default process group")
+        self.rank, self.world_size = dist.get_rank(), dist.get_world_size()
+
+    def all_reduce_(self, t, async_op: bool = False):
+        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=async_op)
+        return work if async_op else t
+
+    def broadcast_(self, t, src=0):
+        dist.broadcast(t, src=src)
+        return t
+
+
+class RcclComm(Communicator):
+    """Native RCCL communicator over xGMI on a dedicated HIP stream."""
+    native = True
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, tag: str | None = None):
+        C = _ext.require()
+        self.rank, self.world_size = rank, world_size
+        if tag is None:
+            tag = str(next(_uid_counter))
+        key = f"pdm_amd/rccl_uid/{tag}"
+        if world_size > 1:
+            store = default_store()
+            if rank == 0:
+                uid = C.rccl_unique_id()
+                store.set(key, uid)
+            else:
+                uid = store.get(key)
+        else:
+            uid = C.rccl_unique_id()
+        self._c = C.RcclComm(bytes(uid), rank, world_size, device.index or 0)
+
+    @property
+    def handle(self):
+        return self._c
+
+    def all_reduce_(self, t):
+        self._c.all_reduce_(t)
+        return t
+
+    def broadcast_(self, t, src=0):
+        self._c.broadcast_(t, src)
+        return t
+
+    def close(self):
+        if self._c is not None:
+            self._c.destroy()
+            self._c = None
+
+
+def make_comm(ctx, force_native: bool = False) -> Communicator:
+    """Pick the data-plane communicator for a rank's DistContext."""
+    if ctx.world_size == 1 and not force_native and not ctx.initialized:
+        return LocalComm()
+    if ctx.is_gpu and ctx.backend == "nccl":
+        return RcclComm(ctx.rank, ctx.world_size, ctx.device)
+    if ctx.initialized:
+        return TorchComm()
+    return LocalComm()

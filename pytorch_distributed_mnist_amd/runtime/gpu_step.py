@@ -1,0 +1,158 @@
+"""GPU step programs: the fixed kernel chains of one training step, and graphs.
+
+Each model family has a ``_train_impl(B)`` that enqueues, on the current HIP
+stream, every kernel of one step plus the bucket all-reduces; it has no host
+inputs (batch indices come from a device step counter), so it is captured once
+per batch size into a ``torch.cuda.CUDAGraph`` (hipGraph) and replayed.
+
+Counter protocol (kernels of one step must not race on a counter): the first
+kernel reads the data-step counter; a *middle* kernel (``lin_reduce`` /
+``cnn_head``) advances both the data-step and the optimizer-step counters; the
+optimizer kernel reads the already-advanced optimizer step (t >= 1).
+
+Linear (reference Net, fp32):  lin_train -> lin_reduce -> [all-reduce] -> optim
+CNN (bf16):  cnn_fwd -> fc1_fwd -> cnn_head -> fc1_bwd -> [all-reduce bucket 0]
+             -> cnn_bwd -> conv_reduce -> [all-reduce bucket 1] -> optim
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import _ext
+
+
+def make_gpu_step(prog, use_graphs: bool = True):
+    if prog.model == "linear":
+        if prog.dtype != "fp32":
+            raise ValueError("the reference Linear model runs in fp32 (--dtype fp32)")
+        return LinearStep(prog, use_graphs)
+    if prog.model == "cnn":
+        if prog.dtype != "bf16":
+            raise ValueError("the CNN GPU path computes in bf16 (--dtype bf16)")
+        from .cnn_step import CnnStep
+        return CnnStep(prog, use_graphs)
+    raise ValueError(prog.model)
+
+
+class GpuStepBase:
+    def __init__(self, prog, use_graphs: bool):
+        self.C = _ext.require()
+        self.prog = prog
+        dev = prog.device
+        self.device = dev
+        self.arena = prog.arena
+        self.opt = prog.optimizer
+        self.reducer = prog.reducer
+        self.train_images = prog.train_split.images.to(dev).contiguous()
+        self.train_labels = prog.train_split.labels.to(device=dev, dtype=torch.int32).contiguous()
+        self.test_images = prog.test_split.images.to(dev).contiguous()
+        self.test_labels = prog.test_split.labels.to(device=dev, dtype=torch.int32).contiguous()
+        # [train data step, (spare)]
+        self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.idx = torch.zeros(0, dtype=torch.int32, device=dev)
+        self.use_graphs = bool(use_graphs) and self.reducer.capturable
+        self.graphs = {}
+        self.bfull = prog.batch_size
+        self.metrics = prog.metrics
+        self._opt_segments = None
+
+    # -- data ----------------------------------------------------------------
+    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
+        """Stream-ordered upload of the next epoch's sample order.
+
+        The copy goes from a pinned staging buffer with non_blocking=True, so the
+        host does not wait for the queued steps of the previous epoch: the copy
+        and the counter reset execute after them, in stream order.  Two staging
+        buffers alternate; an event guards reuse of the older one.
+        """
+        n = idx_cpu.numel()
+        if self.idx.numel() != n:
+            self.idx = torch.empty(n, dtype=torch.int32, device=self.device)
+            self.graphs.clear()          # graphs captured the old buffer address
+            self._staging = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self._staging_ev = [None, None]
+            self._staging_i = 0
+        i = self._staging_i
+        if self._staging_ev[i] is not None:
+            self._staging_ev[i].synchronize()
+        self._staging[i].copy_(idx_cpu.to(torch.int32))
+        self.idx.copy_(self._staging[i], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._staging_ev[i] = ev
+        self._staging_i = 1 - i
+        self.ctr.zero_()
+
+    def begin_epoch(self) -> None:
+        self.opt.sync_hyperparams()
+        self.opt.sync_step()
+
+    # -- step ------------------------------------------------------------------
+    def train_step(self, B: int) -> None:
+        if self.use_graphs:
+            g = self.graphs.get(B)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                # capture on a side stream (torch.cuda.graph's default)
+                with torch.cuda.graph(g):
+                    self._train_impl(B)
+                self.graphs[B] = g
+            g.replay()
+        else:
+            self._train_impl(B)
+        self.opt.step_count += 1
+
+    def _train_impl(self, B: int) -> None:
+        raise NotImplementedError
+
+    # -- optimizer ---------------------------------------------------------------
+    def optimizer_segments(self):
+        """[(offset, rows, cols, shadow|None, shadow_t|None)] covering the arena."""
+        return [(0, 1, self.arena.spec.total, None, None)]
+
+    def launch_optimizer(self) -> None:
+        if self._opt_segments is None:
+            self._opt_segments = self.optimizer_segments()
+        o = self.opt
+        g = o.param_groups[0]
+        if o.kind == "adam":
+            b1, b2 = g["betas"]
+            self.C.optim_step(self.C.OPT_ADAM, self.arena.params, self.arena.grads, o.exp_avg,
+                              o.exp_avg_sq, o._lr_dev, o._step_dev, float(b1), float(b2),
+                              float(g["eps"]), float(g["weight_decay"]), 0.0, 0.0, False,
+                              float(self.reducer.grad_scale), self._opt_segments)
+        else:
+            self.C.optim_step(self.C.OPT_SGD, self.arena.params, self.arena.grads,
+                              o.momentum_buffer, None, o._lr_dev, o._step_dev, 0.0, 0.0, 0.0,
+                              float(g["weight_decay"]), float(g["momentum"]),
+                              float(g["dampening"]), bool(g["nesterov"]),
+                              float(self.reducer.grad_scale), self._opt_segments)
+
+    def invalidate_graphs(self) -> None:
+        self.graphs.clear()
+        self._opt_segments = None
+
+
+class LinearStep(GpuStepBase):
+    def __init__(self, prog, use_graphs):
+        super().__init__(prog, use_graphs)
+        nblk = (self.bfull + self.C.LIN_ROWS - 1) // self.C.LIN_ROWS
+        self.slab = torch.zeros(nblk * self.C.LIN_SLAB, dtype=torch.float32, device=self.device)
+        self.W = self.arena.param("fc.weight")
+        self.b = self.arena.param("fc.bias")
+        self.gW = self.arena.grad("fc.weight")
+        self.gb = self.arena.grad("fc.bias")
+
+    def _train_impl(self, B: int) -> None:
+        C = self.C
+        C.lin_train(self.train_images, self.train_labels, self.idx, self.ctr[0:1], self.bfull, B,
+                    self.W, self.b, self.slab)
+        C.lin_reduce(self.slab, B, self.gW, self.gb, self.metrics.train_view(), self.ctr[0:1],
+                     self.opt._step_dev)
+        self.reducer.bucket_ready(0)
+        self.reducer.finalize()
+        self.launch_optimizer()
+
+    def evaluate(self) -> None:
+        self.C.lin_eval(self.test_images, self.test_labels, self.W, self.b,
+                        self.metrics.eval_view())

@@ -1,0 +1,125 @@
+"""Per-rank training program: device-resident data + step kernels + graphs.
+
+What replaces the reference's DataLoader/Trainer machinery
+(``multi_proc_single_gpu.py:77-161``):
+
+* the uint8 train/test sets are uploaded to the device once (47 + 8 MB);
+* each epoch the rank's DistributedSampler-identical index vector is uploaded
+  (int32, <=240 KB) and a device step counter is reset;
+* a train step is a fixed chain of HIP kernels that read the batch indices via
+  that counter, so the step has no host inputs at all and is captured once per
+  batch size into a hipGraph (``torch.cuda.CUDAGraph`` on ROCm) — the
+  full-batch graph and the ragged-tail graph;
+* loss/accuracy accumulate on the device; the host reads them once per epoch.
+
+On the CPU (gloo path) the same program runs the torch reference step.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..data.sampler import batch_bounds
+from ..utils.metrics import DeviceMetrics
+from .cpu_step import eval_step_cpu, train_step_cpu
+
+
+class TrainProgram:
+    def __init__(self, model: str, dtype: str, arena, optimizer, reducer, train_split, test_split,
+                 batch_size: int, eval_batch: Optional[int] = None, use_graphs: bool = True):
+        self.model = model
+        self.dtype = dtype
+        self.arena = arena
+        self.optimizer = optimizer
+        self.reducer = reducer
+        self.device = arena.device
+        self.batch_size = int(batch_size)
+        if self.batch_size < 1:
+            raise ValueError("per-rank batch size must be >= 1")
+        self.eval_batch = int(eval_batch or self.batch_size)
+        self.metrics = DeviceMetrics(self.device)
+        self.is_gpu = self.device.type == "cuda"
+        self.train_split = train_split
+        self.test_split = test_split
+        self.train_idx_cpu: Optional[torch.Tensor] = None
+        self._bounds = []
+        if self.is_gpu:
+            from .gpu_step import make_gpu_step
+            self.gpu = make_gpu_step(self, use_graphs=use_graphs)
+        else:
+            if dtype != "fp32":
+                raise ValueError("the CPU path computes in fp32 only (--dtype fp32)")
+            self.gpu = None
+
+    # -- epochs ---------------------------------------------------------------
+    def set_train_indices(self, indices: torch.Tensor) -> None:
+        """Install this rank's sample order for the coming epoch."""
+        self.train_idx_cpu = indices.to(torch.int64)
+        self._bounds = batch_bounds(len(indices), self.batch_size)
+        if self.gpu is not None:
+            self.gpu.set_train_indices(self.train_idx_cpu)
+
+    @property
+    def steps_per_epoch(self) -> int:
+        return len(self._bounds)
+
+    def train_epoch(self):
+        self.metrics.reset(DeviceMetrics.TRAIN)
+        self.optimizer.sync_hyperparams()
+        if self.gpu is not None:
+            self.gpu.begin_epoch()
+            for _, size in self._bounds:
+                self.gpu.train_step(size)
+        else:
+            buf = self.metrics.buf[0:3]
+            for start, size in self._bounds:
+                idx = self.train_idx_cpu[start:start + size]
+                train_step_cpu(self.model, self.arena, self.train_split.images[idx],
+                               self.train_split.labels[idx], self.reducer, self.optimizer, buf)
+        return self.metrics.read(DeviceMetrics.TRAIN)
+
+    def run_steps(self, n: int, bsz: Optional[int] = None) -> None:
+        """Run ``n`` full steps from the current counter (bench helper; GPU only)."""
+        for _ in range(n):
+            self.gpu.train_step(bsz or self.batch_size)
+
+    @torch.no_grad()
+    def evaluate(self):
+        """Full, unsharded test-set pass on every rank (reference :99-116, :142-149)."""
+        self.metrics.reset(DeviceMetrics.EVAL)
+        n = len(self.test_split)
+        if self.gpu is not None:
+            self.gpu.evaluate()
+        else:
+            buf = self.metrics.buf[3:6]
+            for start, size in batch_bounds(n, self.eval_batch):
+                eval_step_cpu(self.model, self.arena, self.test_split.images[start:start + size],
+                              self.test_split.labels[start:start + size], buf)
+        return self.metrics.read(DeviceMetrics.EVAL)
+
+
+def build_local_program(arch: str, dtype: str, device, batch_size: int, train_split, test_split,
+                        optimizer: str = "adam", lr: float = 1e-3, momentum: float = 0.9,
+                        weight_decay: float = 1e-4, seed: int = 0, use_graphs: bool = True,
+                        comm=None, force_comm: bool = False):
+    """Single-rank program without a process group (tests, bench at N=1, smoke)."""
+    from types import SimpleNamespace
+
+    from ..models.reference import MODULES
+    from ..models.specs import get_spec
+    from ..optim.flat import build_optimizer
+    from ..parallel.comm import LocalComm
+    from ..parallel.reducer import GradReducer
+    from .arena import FlatArena
+
+    torch.manual_seed(seed)
+    spec = get_spec(arch)
+    arena = FlatArena(spec, torch.device(device))
+    arena.load_module(MODULES[arch]())
+    opt = build_optimizer(optimizer, arena, SimpleNamespace(lr=lr, momentum=momentum,
+                                                            weight_decay=weight_decay))
+    comm = comm or LocalComm()
+    reducer = GradReducer(comm, arena.grads, spec.bucket_bounds(), force=force_comm)
+    return TrainProgram(arch, dtype, arena, opt, reducer, train_split, test_split, batch_size,
+                        use_graphs=use_graphs)
