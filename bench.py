@@ -93,13 +93,17 @@ def main():
         state["epoch"] += 1
         state["step"] = 0
 
+    per_rank = -(-n // ws)
+    full = per_rank // B                       # full-batch steps per epoch
+
     def run(k):
-        full = prog.steps_per_epoch - (1 if (n // ws) % B else 0)   # full-batch steps
-        for _ in range(k):
+        while k > 0:
             if state["step"] >= full:
                 next_epoch()
-            prog.gpu.train_step(B)
-            state["step"] += 1
+            m = min(k, full - state["step"])
+            prog.gpu.train_steps(B, m)
+            state["step"] += m
+            k -= m
 
     opt.sync_hyperparams()
     next_epoch()

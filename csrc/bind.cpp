@@ -176,6 +176,156 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
   launch_optim((int)kind, a, cur_stream(p));
 }
 
+// ------------------------------------------------------------------ CNN (bf16)
+void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* name) {
+  need(t, dt, name);
+  need_numel(t, n, name);
+  need_aligned(t.data_ptr(), 16, name);
+}
+
+void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx,
+             c10::optional<at::Tensor> ctr, int64_t bfull, int64_t B, at::Tensor w1, at::Tensor b1,
+             at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
+             c10::optional<at::Tensor> a1, c10::optional<at::Tensor> xg, at::Tensor ylab) {
+  c10::DeviceGuard g(images.device());
+  const bool gather = idx.has_value() && idx->defined();
+  if (gather) {
+    TORCH_CHECK(ctr.has_value() && ctr->defined(), "ctr required with idx");
+    check_data(images, labels, *idx, *ctr, bfull, B);
+  } else {
+    need(images, at::kByte, "images");
+    need(labels, at::kInt, "labels");
+    TORCH_CHECK(images.dim() == 2 && images.size(1) == 784 && images.size(0) >= B,
+                "images must be [>=B, 784]");
+    need_aligned(images.data_ptr(), 4, "images");
+  }
+  TORCH_CHECK(B >= 1, "B must be >= 1");
+  need(w1, at::kFloat, "w1");
+  need(b1, at::kFloat, "b1");
+  need(b2, at::kFloat, "b2");
+  TORCH_CHECK(w1.numel() == 32 * 9 && b1.numel() == 32 && b2.numel() == 64, "conv1/conv2 bias");
+  need_min(w2, at::kBFloat16, 64 * 288, "w2");
+  need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
+  need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
+  need(ylab, at::kInt, "ylab");
+  need_numel(ylab, B, "ylab");
+  const bool train = a1.has_value() && a1->defined();
+  if (train) {
+    need_min(*a1, at::kBFloat16, B * 676 * 32, "a1");
+    TORCH_CHECK(xg.has_value() && xg->defined(), "xg required in training mode");
+    need_min(*xg, at::kByte, B * 784, "xg");
+  }
+  launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
+                 gather ? idx->data_ptr<int32_t>() : nullptr,
+                 gather ? ctr->data_ptr<int64_t>() : nullptr, (int)bfull, (int)B,
+                 w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2), b2.data_ptr<float>(),
+                 ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(), train ? ptr<__bf16>(*a1) : nullptr,
+                 train ? xg->data_ptr<uint8_t>() : nullptr, ylab.data_ptr<int32_t>(),
+                 cur_stream(images));
+}
+
+void fc1_fwd(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_t splitk) {
+  c10::DeviceGuard g(pool.device());
+  TORCH_CHECK(B >= 1, "B must be >= 1");
+  TORCH_CHECK(splitk >= 1 && (CNN_FEAT / 32) % splitk == 0, "splitk must divide 288");
+  need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
+  need_min(wf1, at::kBFloat16, (int64_t)CNN_HID * CNN_FEAT, "wf1");
+  need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
+  launch_fc1_fwd(ptr<__bf16>(pool), ptr<__bf16>(wf1), part.data_ptr<float>(), (int)B, (int)splitk,
+                 cur_stream(pool));
+}
+
+void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Tensor wf2,
+              at::Tensor bf2, at::Tensor ylab, bool train, c10::optional<at::Tensor> dh,
+              c10::optional<at::Tensor> dht, int64_t ldt, c10::optional<at::Tensor> slab,
+              at::Tensor metrics, c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1) {
+  c10::DeviceGuard g(part.device());
+  TORCH_CHECK(B >= 1, "B must be >= 1");
+  need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
+  need_min(bf1, at::kFloat, CNN_HID, "bf1");
+  need_min(wf2, at::kFloat, CNN_NCLS * CNN_HID, "wf2");
+  need(bf2, at::kFloat, "bf2");
+  TORCH_CHECK(bf2.numel() == CNN_NCLS, "bf2");
+  need(ylab, at::kInt, "ylab");
+  need_numel(ylab, B, "ylab");
+  need(metrics, at::kDouble, "metrics");
+  need_numel(metrics, 3, "metrics");
+  __bf16 *pdh = nullptr, *pdht = nullptr;
+  float* pslab = nullptr;
+  if (train) {
+    TORCH_CHECK(ldt % 32 == 0 && ldt >= B, "ldt must be a multiple of 32 and >= B");
+    TORCH_CHECK(dh && dht && slab, "train mode needs dh, dht, slab");
+    need_min(*dh, at::kBFloat16, ldt * CNN_HID, "dh");
+    need_min(*dht, at::kBFloat16, ldt * CNN_HID, "dht");
+    need_min(*slab, at::kFloat, (ldt / CNN_HEAD_ROWS) * CNN_HEAD_SLAB, "head slab");
+    pdh = ptr<__bf16>(*dh);
+    pdht = ptr<__bf16>(*dht);
+    pslab = slab->data_ptr<float>();
+  }
+  launch_cnn_head(part.data_ptr<float>(), (int)splitk, (int)B, bf1.data_ptr<float>(),
+                  wf2.data_ptr<float>(), bf2.data_ptr<float>(), ylab.data_ptr<int32_t>(), train, pdh,
+                  pdht, (int)ldt, pslab, metrics.data_ptr<double>(), opt_i64(c0), opt_i64(c1),
+                  cur_stream(part));
+}
+
+void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Tensor wf1t,
+             int64_t B, at::Tensor gwf1, at::Tensor dpool, at::Tensor head_slab, at::Tensor gwf2,
+             at::Tensor gbf2, at::Tensor gbf1, at::Tensor metrics) {
+  c10::DeviceGuard g(dh.device());
+  TORCH_CHECK(B >= 1 && ldt % 32 == 0 && ldt >= B, "bad ldt/B");
+  need_min(dh, at::kBFloat16, ldt * CNN_HID, "dh");
+  need_min(dht, at::kBFloat16, ldt * CNN_HID, "dht");
+  need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
+  need_min(wf1t, at::kBFloat16, (int64_t)CNN_FEAT * CNN_HID, "wf1t");
+  need_min(dpool, at::kBFloat16, B * CNN_FEAT, "dpool");
+  need(gwf1, at::kFloat, "gwf1");
+  need(gwf2, at::kFloat, "gwf2");
+  need(gbf2, at::kFloat, "gbf2");
+  need(gbf1, at::kFloat, "gbf1");
+  TORCH_CHECK(gwf1.numel() == (int64_t)CNN_HID * CNN_FEAT && gwf2.numel() == CNN_NCLS * CNN_HID &&
+                  gbf2.numel() == CNN_NCLS && gbf1.numel() == CNN_HID, "fc grad views");
+  const int64_t hb = ldt / CNN_HEAD_ROWS;
+  need_min(head_slab, at::kFloat, hb * CNN_HEAD_SLAB, "head slab");
+  need(metrics, at::kDouble, "metrics");
+  need_numel(metrics, 3, "metrics");
+  launch_fc1_bwd(ptr<__bf16>(dh), ptr<__bf16>(dht), (int)ldt, ptr<__bf16>(pool), ptr<__bf16>(wf1t),
+                 (int)B, gwf1.data_ptr<float>(), ptr<__bf16>(dpool), head_slab.data_ptr<float>(),
+                 (int)hb, gwf2.data_ptr<float>(), gbf2.data_ptr<float>(), gbf1.data_ptr<float>(),
+                 metrics.data_ptr<double>(), cur_stream(dh));
+}
+
+void cnn_bwd(at::Tensor xg, at::Tensor a1, at::Tensor dpool, at::Tensor pmask, at::Tensor w2t,
+             int64_t B, int64_t ipb, at::Tensor slab) {
+  c10::DeviceGuard g(xg.device());
+  TORCH_CHECK(B >= 1 && ipb >= 1, "bad B/ipb");
+  need_min(xg, at::kByte, B * 784, "xg");
+  need_min(a1, at::kBFloat16, B * 676 * 32, "a1");
+  need_min(dpool, at::kBFloat16, B * CNN_FEAT, "dpool");
+  need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
+  need_min(w2t, at::kBFloat16, 288 * 64, "w2t");
+  need_min(slab, at::kFloat, (int64_t)cnn_bwd_blocks((int)B, (int)ipb) * CNN_CONV_SLAB, "conv slab");
+  launch_cnn_bwd(xg.data_ptr<uint8_t>(), ptr<__bf16>(a1), ptr<__bf16>(dpool),
+                 pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
+                 slab.data_ptr<float>(), cur_stream(xg));
+}
+
+void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, at::Tensor gw1,
+                 at::Tensor gb1) {
+  c10::DeviceGuard g(slab.device());
+  need_min(slab, at::kFloat, nblk * CNN_CONV_SLAB, "conv slab");
+  need(gw2, at::kFloat, "gw2");
+  need(gb2, at::kFloat, "gb2");
+  need(gw1, at::kFloat, "gw1");
+  need(gb1, at::kFloat, "gb1");
+  TORCH_CHECK(gw2.numel() == 64 * 288 && gb2.numel() == 64 && gw1.numel() == 288 &&
+                  gb1.numel() == 32, "conv grad views");
+  launch_conv_reduce(slab.data_ptr<float>(), (int)nblk, gw2.data_ptr<float>(),
+                     gb2.data_ptr<float>(), gw1.data_ptr<float>(), gb1.data_ptr<float>(),
+                     cur_stream(slab));
+}
+
+int64_t cnn_bwd_nblk(int64_t B, int64_t ipb) { return cnn_bwd_blocks((int)B, (int)ipb); }
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -188,5 +338,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("lin_reduce", &lin_reduce);
   m.def("lin_eval", &lin_eval);
   m.def("optim_step", &optim_step);
+  m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
+  m.attr("CNN_HEAD_SLAB") = CNN_HEAD_SLAB;
+  m.attr("CNN_CONV_SLAB") = CNN_CONV_SLAB;
+  m.def("cnn_fwd", &cnn_fwd);
+  m.def("fc1_fwd", &fc1_fwd);
+  m.def("cnn_head", &cnn_head);
+  m.def("fc1_bwd", &fc1_bwd);
+  m.def("cnn_bwd", &cnn_bwd);
+  m.def("conv_reduce", &conv_reduce);
+  m.def("cnn_bwd_nblk", &cnn_bwd_nblk);
   register_comm(m);
 }

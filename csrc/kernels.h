@@ -78,7 +78,8 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
                      hipStream_t st);
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
-                    int head_blocks, float* gwf2, float* gbf2, float* gbf1, hipStream_t st);
+                    int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
+                    hipStream_t st);
 void launch_cnn_bwd(const uint8_t* xg, const __bf16* a1, const __bf16* dpool, const uint8_t* pmask,
                     const __bf16* w2t, int B, int imgs_per_block, float* slab, hipStream_t st);
 int cnn_bwd_blocks(int B, int imgs_per_block);

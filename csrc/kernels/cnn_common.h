@@ -1,0 +1,70 @@
+// Shapes, LDS image layouts and small helpers shared by the CNN kernels.
+#pragma once
+#include "../common.h"
+#include "../kernels.h"
+
+namespace cnn {
+
+constexpr int IMG = 28;               // input 28x28
+constexpr int C1 = 32, H1 = 26, P1 = H1 * H1;   // conv1 out 26x26x32
+constexpr int C2 = 64, H2 = 24, P2 = H2 * H2;   // conv2 out 24x24x64
+constexpr int HP = 12, PP = HP * HP;            // pooled 12x12x64
+constexpr int FEAT = CNN_FEAT;        // 9216
+constexpr int HID = CNN_HID;          // 128
+constexpr int NCLS = CNN_NCLS;        // 10
+constexpr int HEAD_ROWS = CNN_HEAD_ROWS;
+constexpr int HEAD_SLAB = CNN_HEAD_SLAB;
+constexpr int CONV_SLAB = CNN_CONV_SLAB;
+
+// LDS image of a1 (26x26 pixels x 32 bf16 = 64 B/pixel).  The 16-B chunk index is
+// XOR-swizzled with (col & 3): with the conv2 A-fragment pattern (4 pooled pixels x
+// 2x2 windows, ds_read_b128) every 16-lane group then hits 16 distinct 16-B slots
+// (conflict-free; plain layout is 2-way), and the wgrad transposed reads stay <= 2-way.
+__device__ __forceinline__ int a1_off(int row, int col, int byte) {
+  return (row * H1 + col) * 64 + ((((byte >> 4) ^ (col & 3))) << 4) + (byte & 15);
+}
+
+// LDS image of dz2 = dL/d(conv2 pre-activation) (24x24 x 64 bf16 = 128 B/pixel).
+// Chunk swizzle (2*row + col) & 7: conflict-free ds_read_b128 for the dgrad A rows,
+// 2-way for the wgrad ds_read_b64_tr_b16 column reads (searched, see docs/kernels.md).
+__device__ __forceinline__ int dz_off(int row, int col, int byte) {
+  return (row * H2 + col) * 128 + ((((byte >> 4) ^ ((2 * row + col) & 7))) << 4) + (byte & 15);
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group gives the address of row q,
+// columns 4p..4p+3; lane i receives column i of the 4 rows.
+__device__ __forceinline__ s16x4 lds_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int N>
+__device__ __forceinline__ float row_xent(const float (&lg)[N], int y, float (&p)[N], int& correct) {
+  float m = lg[0];
+  int am = 0;
+#pragma unroll
+  for (int n = 1; n < N; ++n)
+    if (lg[n] > m) { m = lg[n]; am = n; }
+  float s = 0.f;
+#pragma unroll
+  for (int n = 0; n < N; ++n) { p[n] = expf(lg[n] - m); s += p[n]; }
+  const float lse = m + logf(s);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] *= inv;
+  correct = (am == y);
+  float ly = lg[0];
+#pragma unroll
+  for (int n = 1; n < N; ++n) ly = (n == y) ? lg[n] : ly;
+  return lse - ly;
+}
+
+}  // namespace cnn

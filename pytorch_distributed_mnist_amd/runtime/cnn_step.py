@@ -1,0 +1,141 @@
+"""CNN (bf16) GPU step program.
+
+Kernel chain of one training step (all on the compute stream; the two bucket
+all-reduces fork onto the RCCL stream):
+
+  cnn_fwd      gather+normalise, conv1+ReLU, conv2+ReLU+maxpool  -> pool, mask, a1, x
+  fc1_fwd      split-K fc1 GEMM                                  -> fp32 partials
+  cnn_head     fc1 reduce+bias+ReLU, fc2, CE, head backward      -> dh, dh^T, head slabs
+               (advances the data-step and optimizer-step counters)
+  fc1_bwd      dW1 tiles | dX tiles | head-slab reduce           -> bucket 0 complete
+  [all-reduce bucket 0 on the comm stream, overlapping the next two kernels]
+  cnn_bwd      conv2 wgrad | conv2 dgrad + conv1 wgrad           -> conv slabs
+  conv_reduce  fixed-order slab sum                              -> bucket 1 complete
+  [all-reduce bucket 1]
+  optim        SGD/Adam over the arena + bf16 weight copies (W1, W1^T, W2, W2^T)
+
+Evaluation runs cnn_fwd (no activations kept) -> fc1_fwd -> cnn_head over the
+whole test set in chunks of EVAL_CHUNK images.
+"""
+from __future__ import annotations
+
+import torch
+
+from .gpu_step import GpuStepBase
+
+EVAL_CHUNK = 2048
+
+
+def choose_splitk(B: int, cap: int = 16, target_blocks: int = 256) -> int:
+    """Split-K factor for fc1_fwd: a divisor of 288 (K-steps of 32) giving ~target blocks."""
+    mtiles = (B + 31) // 32
+    best = 1
+    for s in (1, 2, 3, 4, 6, 8, 9, 12, 16, 18, 24, 32):
+        if s <= cap and mtiles * s <= target_blocks:
+            best = s
+    return best
+
+
+def choose_ipb(B: int, cus: int = 256) -> int:
+    """Images per cnn_bwd workgroup: one workgroup per CU once B exceeds the CU count."""
+    return max(1, -(-B // cus))
+
+
+class CnnStep(GpuStepBase):
+    def __init__(self, prog, use_graphs):
+        super().__init__(prog, use_graphs)
+        C, dev, B = self.C, self.device, self.bfull
+        a = self.arena
+        bf16 = torch.bfloat16
+        self.ldt = -(-B // 32) * 32
+        cap = max(B, EVAL_CHUNK)
+        # activations / workspaces (sized once; graphs capture their addresses)
+        self.pool = torch.empty(cap * 9216, dtype=bf16, device=dev)
+        self.pmask = torch.empty(cap * 9216, dtype=torch.uint8, device=dev)
+        self.a1 = torch.empty(B * 676 * 32, dtype=bf16, device=dev)
+        self.xg = torch.empty(B * 784, dtype=torch.uint8, device=dev)
+        self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.splitk_train = choose_splitk(B)
+        self.splitk_eval = choose_splitk(min(cap, EVAL_CHUNK))
+        part_n = max(self.splitk_train * B, self.splitk_eval * EVAL_CHUNK) * 128
+        self.part = torch.empty(part_n, dtype=torch.float32, device=dev)
+        self.dh = torch.zeros(self.ldt * 128, dtype=bf16, device=dev)
+        self.dht = torch.zeros(self.ldt * 128, dtype=bf16, device=dev)
+        self.head_slab = torch.empty((self.ldt // 16) * C.CNN_HEAD_SLAB, dtype=torch.float32,
+                                     device=dev)
+        self.dpool = torch.empty(B * 9216, dtype=bf16, device=dev)
+        self.ipb = choose_ipb(B)
+        self.conv_nblk = C.cnn_bwd_nblk(B, self.ipb)
+        self.conv_slab = torch.empty(self.conv_nblk * C.CNN_CONV_SLAB, dtype=torch.float32,
+                                     device=dev)
+        # bf16 compute copies of the weights (kept current by the optimizer kernel)
+        self.wf1 = torch.empty(128 * 9216, dtype=bf16, device=dev)
+        self.wf1t = torch.empty(9216 * 128, dtype=bf16, device=dev)
+        self.w2 = torch.empty(64 * 288, dtype=bf16, device=dev)
+        self.w2t = torch.empty(288 * 64, dtype=bf16, device=dev)
+        # parameter / gradient views (kernel layouts)
+        p, g = a.param, a.grad
+        self.P = {n: p(n) for n in ("conv1.weight", "conv1.bias", "conv2.bias", "fc1.bias",
+                                    "fc2.weight", "fc2.bias")}
+        self.G = {n: g(n) for n in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias",
+                                    "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")}
+        self.refresh_shadows()
+
+    @torch.no_grad()
+    def refresh_shadows(self) -> None:
+        """Re-derive the bf16 weight copies from the fp32 master weights."""
+        w1 = self.arena.param("fc1.weight").reshape(128, 9216)
+        self.wf1.copy_(w1.reshape(-1).to(torch.bfloat16))
+        self.wf1t.copy_(w1.t().contiguous().reshape(-1).to(torch.bfloat16))
+        w2 = self.arena.param("conv2.weight").reshape(64, 288)
+        self.w2.copy_(w2.reshape(-1).to(torch.bfloat16))
+        self.w2t.copy_(w2.t().contiguous().reshape(-1).to(torch.bfloat16))
+
+    def optimizer_segments(self):
+        spec = self.arena.spec
+        segs = []
+        for p in spec.params:
+            off = spec.offset(p.name)
+            if p.name == "fc1.weight":
+                segs.append((off, 128, 9216, self.wf1, self.wf1t))
+            elif p.name == "conv2.weight":
+                segs.append((off, 64, 288, self.w2, self.w2t))
+            else:
+                segs.append((off, 1, p.numel, None, None))
+        return segs
+
+    def _train_impl(self, B: int) -> None:
+        C, P, G = self.C, self.P, self.G
+        ldt = -(-B // 32) * 32
+        S = self.splitk_train
+        C.cnn_fwd(self.train_images, self.train_labels, self.idx, self.ctr[0:1], self.bfull, B,
+                  P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
+                  self.pmask, self.a1, self.xg, self.ylab)
+        C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
+        C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab, True,
+                   self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
+                   self.ctr[0:1], self.opt._step_dev)
+        C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
+                  self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
+                  self.metrics.train_view())
+        self.reducer.bucket_ready(0)
+        ipb = choose_ipb(B)
+        C.cnn_bwd(self.xg, self.a1, self.dpool, self.pmask, self.w2t, B, ipb, self.conv_slab)
+        C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
+                      G["conv1.weight"], G["conv1.bias"])
+        self.reducer.bucket_ready(1)
+        self.reducer.finalize()
+        self.launch_optimizer()
+
+    def evaluate(self) -> None:
+        C, P = self.C, self.P
+        n = self.test_images.shape[0]
+        S = self.splitk_eval
+        for s in range(0, n, EVAL_CHUNK):
+            b = min(EVAL_CHUNK, n - s)
+            C.cnn_fwd(self.test_images[s:s + b], self.test_labels[s:s + b], None, None, b, b,
+                      P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
+                      self.pmask, None, None, self.ylab)
+            C.fc1_fwd(self.pool, self.wf1, self.part, b, S)
+            C.cnn_head(self.part, S, b, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
+                       False, None, None, 32, None, self.metrics.eval_view(), None, None)

@@ -88,19 +88,45 @@ class GpuStepBase:
         self.opt.sync_step()
 
     # -- step ------------------------------------------------------------------
-    def train_step(self, B: int) -> None:
-        if self.use_graphs:
-            g = self.graphs.get(B)
-            if g is None:
-                g = torch.cuda.CUDAGraph()
-                # capture on a side stream (torch.cuda.graph's default)
-                with torch.cuda.graph(g):
+    # One hipGraph replay costs ~10-16 us of host time (MI355X_MICROARCH.md price
+    # list, graph-replay-floor) — more than a whole small step's GPU time — so
+    # steps are captured GRAPH_STEPS at a time (identical steps: the batch comes
+    # from the device counter) and a run of n steps replays n // GRAPH_STEPS
+    # multi-step graphs plus single-step graphs for the remainder.
+    GRAPH_STEPS = 8
+
+    def _graph(self, B: int, nsteps: int):
+        key = (B, nsteps)
+        g = self.graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):          # captured on a side stream
+                for _ in range(nsteps):
                     self._train_impl(B)
-                self.graphs[B] = g
-            g.replay()
+            self.graphs[key] = g
+        return g
+
+    def train_steps(self, B: int, n: int) -> None:
+        """Enqueue n consecutive training steps of batch size B."""
+        if n <= 0:
+            return
+        if self.use_graphs:
+            k = self.GRAPH_STEPS
+            if n >= k:
+                gk = self._graph(B, k)
+                for _ in range(n // k):
+                    gk.replay()
+            if n % k:
+                g1 = self._graph(B, 1)
+                for _ in range(n % k):
+                    g1.replay()
         else:
-            self._train_impl(B)
-        self.opt.step_count += 1
+            for _ in range(n):
+                self._train_impl(B)
+        self.opt.step_count += n
+
+    def train_step(self, B: int) -> None:
+        self.train_steps(B, 1)
 
     def _train_impl(self, B: int) -> None:
         raise NotImplementedError

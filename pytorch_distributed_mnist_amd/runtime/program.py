@@ -69,8 +69,11 @@ class TrainProgram:
         self.optimizer.sync_hyperparams()
         if self.gpu is not None:
             self.gpu.begin_epoch()
-            for _, size in self._bounds:
-                self.gpu.train_step(size)
+            sizes = [size for _, size in self._bounds]
+            full = sum(1 for s in sizes if s == self.batch_size)
+            self.gpu.train_steps(self.batch_size, full)      # full batches come first
+            for s in sizes[full:]:
+                self.gpu.train_step(s)                        # ragged tail
         else:
             buf = self.metrics.buf[0:3]
             for start, size in self._bounds:
@@ -81,8 +84,7 @@ class TrainProgram:
 
     def run_steps(self, n: int, bsz: Optional[int] = None) -> None:
         """Run ``n`` full steps from the current counter (bench helper; GPU only)."""
-        for _ in range(n):
-            self.gpu.train_step(bsz or self.batch_size)
+        self.gpu.train_steps(bsz or self.batch_size, n)
 
     @torch.no_grad()
     def evaluate(self):
