@@ -385,22 +385,23 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
                                                           float* __restrict__ gb2,
                                                           float* __restrict__ gw1,
                                                           float* __restrict__ gb1) {
-  __shared__ float part[4][64];
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int grp = threadIdx.x >> 6;
-  float s = 0.f;
-  if (e < CONV_SLAB)
-    for (int j = grp; j < nblk; j += 4) s += slab[(int64_t)j * CONV_SLAB + e];
-  part[grp][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (threadIdx.x < 64 && e < CONV_SLAB) {
-    const float t = (part[0][threadIdx.x] + part[1][threadIdx.x]) +
-                    (part[2][threadIdx.x] + part[3][threadIdx.x]);
-    if (e < SL_DB2) gw2[e] = t;
-    else if (e < SL_DW1) gb2[e - SL_DB2] = t;
-    else if (e < SL_DB1) gw1[e - SL_DW1] = t;
-    else gb1[e - SL_DB1] = t;
+  // block = 256 consecutive slab columns; each thread sums every slab for 1 column with
+  // 8 independent accumulators (8 loads in flight), fixed order -> deterministic.
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= CONV_SLAB) return;
+  const float* p = slab + e;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int j = 0;
+  for (; j + 8 <= nblk; j += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += p[(int64_t)(j + u) * CONV_SLAB];
   }
+  for (; j < nblk; ++j) acc[0] += p[(int64_t)j * CONV_SLAB];
+  const float t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (e < SL_DB2) gw2[e] = t;
+  else if (e < SL_DW1) gb2[e - SL_DB2] = t;
+  else if (e < SL_DB1) gw1[e - SL_DW1] = t;
+  else gb1[e - SL_DB1] = t;
 }
 
 }  // namespace
@@ -424,5 +425,5 @@ void launch_cnn_bwd(const uint8_t* xg, const __bf16* a1, const __bf16* dpool, co
 
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st) {
-  conv_reduce_kernel<<<(CONV_SLAB + 63) / 64, 256, 0, st>>>(slab, nblk, gw2, gb2, gw1, gb1);
+  conv_reduce_kernel<<<(CONV_SLAB + 255) / 256, 256, 0, st>>>(slab, nblk, gw2, gb2, gw1, gb1);
 }

@@ -123,37 +123,75 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     return;
   }
 
-  // transposed-shadow segment: tile of TR rows x TC cols
-  __shared__ bf16 tile[TC][TR + 2];
+  // transposed-shadow segment: tile of TR rows x TC cols.  Thread -> (row, 8 consecutive
+  // cols): every fp32 load/store is a float4 and a row's 64 columns are 256 contiguous
+  // bytes; the bf16 values are staged in LDS and written transposed as 16-B stores.
+  __shared__ __attribute__((aligned(16))) bf16 tile[TC][TR + 8];
   const int tiles_c = (s.cols + TC - 1) / TC;
   const int tr0 = (lb / tiles_c) * TR, tc0 = (lb % tiles_c) * TC;
-  // thread -> (row r, cols c..c+7): 32 rows x 8 col-groups = 256 threads
-  const int r = threadIdx.x >> 3, cg = (threadIdx.x & 7) * 8;
-  const int row = tr0 + r;
+  const int r = threadIdx.x >> 3, c8 = (threadIdx.x & 7) * 8;
+  const int row = tr0 + r, col0 = tc0 + c8;
+  if (row < s.rows && col0 < s.cols) {
+    const int64_t e = (int64_t)row * s.cols + col0;
+    if (col0 + 8 <= s.cols && (e & 3) == 0) {
+      float pv[8], gv[8], mv[8], vv[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = tc0 + cg + j;
-    if (row < s.rows && col < s.cols) {
-      const int64_t e = (int64_t)row * s.cols + col;
-      float m = M[e], v = (KIND == OPT_ADAM) ? V[e] : 0.f;
-      const float p = update<KIND>(P[e], G[e], m, v, h, a.grad_scale);
-      P[e] = p;
-      M[e] = m;
-      if (KIND == OPT_ADAM) V[e] = v;
-      const bf16 hb = to_bf16(p);
-      if (s.shadow) s.shadow[e] = hb;
-      tile[cg + j][r] = hb;
+      for (int q = 0; q < 2; ++q) {
+        const float4 p4 = *reinterpret_cast<const float4*>(P + e + 4 * q);
+        const float4 g4 = *reinterpret_cast<const float4*>(G + e + 4 * q);
+        const float4 m4 = *reinterpret_cast<const float4*>(M + e + 4 * q);
+        pv[4 * q] = p4.x; pv[4 * q + 1] = p4.y; pv[4 * q + 2] = p4.z; pv[4 * q + 3] = p4.w;
+        gv[4 * q] = g4.x; gv[4 * q + 1] = g4.y; gv[4 * q + 2] = g4.z; gv[4 * q + 3] = g4.w;
+        mv[4 * q] = m4.x; mv[4 * q + 1] = m4.y; mv[4 * q + 2] = m4.z; mv[4 * q + 3] = m4.w;
+        if (KIND == OPT_ADAM) {
+          const float4 v4 = *reinterpret_cast<const float4*>(V + e + 4 * q);
+          vv[4 * q] = v4.x; vv[4 * q + 1] = v4.y; vv[4 * q + 2] = v4.z; vv[4 * q + 3] = v4.w;
+        } else {
+          vv[4 * q] = vv[4 * q + 1] = vv[4 * q + 2] = vv[4 * q + 3] = 0.f;
+        }
+      }
+      bf16x8 hb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pv[j] = update<KIND>(pv[j], gv[j], mv[j], vv[j], h, a.grad_scale);
+        hb[j] = to_bf16(pv[j]);
+        tile[c8 + j][r] = hb[j];
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        *reinterpret_cast<float4*>(P + e + 4 * q) =
+            make_float4(pv[4 * q], pv[4 * q + 1], pv[4 * q + 2], pv[4 * q + 3]);
+        *reinterpret_cast<float4*>(M + e + 4 * q) =
+            make_float4(mv[4 * q], mv[4 * q + 1], mv[4 * q + 2], mv[4 * q + 3]);
+        if (KIND == OPT_ADAM)
+          *reinterpret_cast<float4*>(V + e + 4 * q) =
+              make_float4(vv[4 * q], vv[4 * q + 1], vv[4 * q + 2], vv[4 * q + 3]);
+      }
+      if (s.shadow) *reinterpret_cast<bf16x8*>(s.shadow + e) = hb;
+    } else {
+      for (int j = 0; j < 8 && col0 + j < s.cols; ++j) {
+        const int64_t ej = e + j;
+        float m = M[ej], v = (KIND == OPT_ADAM) ? V[ej] : 0.f;
+        const float p = update<KIND>(P[ej], G[ej], m, v, h, a.grad_scale);
+        P[ej] = p;
+        M[ej] = m;
+        if (KIND == OPT_ADAM) V[ej] = v;
+        const bf16 hb = to_bf16(p);
+        if (s.shadow) s.shadow[ej] = hb;
+        tile[c8 + j][r] = hb;
+      }
     }
   }
   __syncthreads();
-  // write transposed: shadow_t[col][row]; thread -> (col c, rows rr..rr+3)
+  // transposed store: thread -> (col c, 8 consecutive rows) = one 16-B store
   const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 8;
   const int col = tc0 + c;
   if (col < s.cols) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int rw = tr0 + rr + j;
-      if (rw < s.rows) s.shadow_t[(int64_t)col * s.rows + rw] = tile[c][rr + j];
+    const int64_t base = (int64_t)col * s.rows + tr0 + rr;
+    if (tr0 + rr + 8 <= s.rows && (base & 7) == 0) {
+      *reinterpret_cast<bf16x8*>(s.shadow_t + base) = *reinterpret_cast<const bf16x8*>(&tile[c][rr]);
+    } else {
+      for (int j = 0; j < 8 && tr0 + rr + j < s.rows; ++j) s.shadow_t[base + j] = tile[c][rr + j];
     }
   }
 }
