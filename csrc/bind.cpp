@@ -70,7 +70,7 @@ void lin_train(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tensor 
   need_numel(slab, nblk * LIN_SLAB, "slab");
   need_aligned(slab.data_ptr(), 16, "slab");
   launch_lin_train(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
-                   ctr.data_ptr<int64_t>(), (int)bfull, (int)B, W.data_ptr<float>(),
+                   idx.numel(), ctr.data_ptr<int64_t>(), (int)bfull, (int)B, W.data_ptr<float>(),
                    b.data_ptr<float>(), slab.data_ptr<float>(), cur_stream(images));
 }
 
@@ -107,6 +107,26 @@ void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
   launch_lin_eval(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), (int)images.size(0),
                   W.data_ptr<float>(), b.data_ptr<float>(), metrics.data_ptr<double>(),
                   cur_stream(images));
+}
+
+// ------------------------------------------------------------------ data
+void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tensor out_images,
+                  at::Tensor out_labels) {
+  c10::DeviceGuard g(images.device());
+  need(images, at::kByte, "images");
+  need(labels, at::kInt, "labels");
+  need(idx, at::kInt, "idx");
+  need(out_images, at::kByte, "out_images");
+  need(out_labels, at::kInt, "out_labels");
+  TORCH_CHECK(images.dim() == 2 && images.size(1) == 784, "images must be [N, 784]");
+  const int64_t n = idx.numel();
+  TORCH_CHECK(out_images.numel() >= n * 784 && out_labels.numel() >= n, "output too small");
+  need_aligned(images.data_ptr(), 16, "images");
+  need_aligned(out_images.data_ptr(), 16, "out_images");
+  // indices are validated on the host by the caller (sampler output < N)
+  launch_gather_epoch(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
+                      idx.data_ptr<int32_t>(), (int)n, out_images.data_ptr<uint8_t>(),
+                      out_labels.data_ptr<int32_t>(), cur_stream(images));
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -186,12 +206,21 @@ void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* nam
 void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx,
              c10::optional<at::Tensor> ctr, int64_t bfull, int64_t B, at::Tensor w1, at::Tensor b1,
              at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
-             c10::optional<at::Tensor> a1, c10::optional<at::Tensor> xg, at::Tensor ylab) {
+             c10::optional<at::Tensor> xg, at::Tensor ylab) {
   c10::DeviceGuard g(images.device());
   const bool gather = idx.has_value() && idx->defined();
+  const bool counted = ctr.has_value() && ctr->defined();
   if (gather) {
-    TORCH_CHECK(ctr.has_value() && ctr->defined(), "ctr required with idx");
+    TORCH_CHECK(counted, "ctr required with idx");
     check_data(images, labels, *idx, *ctr, bfull, B);
+  } else if (counted) {
+    // epoch buffer mode: rows [ctr*bfull, ctr*bfull + B) of images (host keeps ctr in range)
+    need(images, at::kByte, "images");
+    need(labels, at::kInt, "labels");
+    need(*ctr, at::kLong, "ctr");
+    TORCH_CHECK(images.dim() == 2 && images.size(1) == 784 && images.size(0) >= B, "images");
+    TORCH_CHECK(B >= 1 && B <= bfull, "batch must be in [1, bfull]");
+    need_aligned(images.data_ptr(), 4, "images");
   } else {
     need(images, at::kByte, "images");
     need(labels, at::kInt, "labels");
@@ -209,17 +238,13 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
   need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
   need(ylab, at::kInt, "ylab");
   need_numel(ylab, B, "ylab");
-  const bool train = a1.has_value() && a1->defined();
-  if (train) {
-    need_min(*a1, at::kBFloat16, B * 676 * 32, "a1");
-    TORCH_CHECK(xg.has_value() && xg->defined(), "xg required in training mode");
-    need_min(*xg, at::kByte, B * 784, "xg");
-  }
+  const bool train = xg.has_value() && xg->defined();
+  if (train) need_min(*xg, at::kByte, B * 784, "xg");
   launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
                  gather ? idx->data_ptr<int32_t>() : nullptr,
-                 gather ? ctr->data_ptr<int64_t>() : nullptr, (int)bfull, (int)B,
+                 gather ? idx->numel() : images.size(0), counted ? ctr->data_ptr<int64_t>() : nullptr, (int)bfull, (int)B,
                  w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2), b2.data_ptr<float>(),
-                 ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(), train ? ptr<__bf16>(*a1) : nullptr,
+                 ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(),
                  train ? xg->data_ptr<uint8_t>() : nullptr, ylab.data_ptr<int32_t>(),
                  cur_stream(images));
 }
@@ -294,18 +319,20 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
                  metrics.data_ptr<double>(), cur_stream(dh));
 }
 
-void cnn_bwd(at::Tensor xg, at::Tensor a1, at::Tensor dpool, at::Tensor pmask, at::Tensor w2t,
-             int64_t B, int64_t ipb, at::Tensor slab) {
+void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::Tensor pmask,
+             at::Tensor w2t, int64_t B, int64_t ipb, at::Tensor slab) {
   c10::DeviceGuard g(xg.device());
   TORCH_CHECK(B >= 1 && ipb >= 1, "bad B/ipb");
   need_min(xg, at::kByte, B * 784, "xg");
-  need_min(a1, at::kBFloat16, B * 676 * 32, "a1");
+  need(w1, at::kFloat, "w1");
+  need(b1, at::kFloat, "b1");
+  TORCH_CHECK(w1.numel() == 32 * 9 && b1.numel() == 32, "conv1 weight/bias");
   need_min(dpool, at::kBFloat16, B * CNN_FEAT, "dpool");
   need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
   need_min(w2t, at::kBFloat16, 288 * 64, "w2t");
   need_min(slab, at::kFloat, (int64_t)cnn_bwd_blocks((int)B, (int)ipb) * CNN_CONV_SLAB, "conv slab");
-  launch_cnn_bwd(xg.data_ptr<uint8_t>(), ptr<__bf16>(a1), ptr<__bf16>(dpool),
-                 pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
+  launch_cnn_bwd(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
+                 ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
                  slab.data_ptr<float>(), cur_stream(xg));
 }
 
@@ -326,6 +353,14 @@ void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, 
 
 int64_t cnn_bwd_nblk(int64_t B, int64_t ipb) { return cnn_bwd_blocks((int)B, (int)ipb); }
 
+at::Tensor read_stamps(const std::string& which) {
+  at::Tensor t = at::zeros({256, 16}, at::TensorOptions().dtype(at::kLong));
+  auto* p = reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>());
+  if (which == "fwd") read_stamps_fwd(p);
+  else read_stamps_bwd(p);
+  return t;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -338,6 +373,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lin_reduce", &lin_reduce);
   m.def("lin_eval", &lin_eval);
   m.def("optim_step", &optim_step);
+  m.def("gather_epoch", &gather_epoch);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
   m.attr("CNN_HEAD_SLAB") = CNN_HEAD_SLAB;
   m.attr("CNN_CONV_SLAB") = CNN_CONV_SLAB;
@@ -348,5 +384,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_bwd", &cnn_bwd);
   m.def("conv_reduce", &conv_reduce);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk);
+  m.def("read_stamps", &read_stamps);
   register_comm(m);
 }

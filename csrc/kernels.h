@@ -12,12 +12,16 @@ constexpr int LIN_ROWS = 8;
 constexpr int LIN_SLAB = 7856;  // 7840 dW + 10 db + loss + correct, padded
 
 void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                      const int64_t* ctr, int bfull, int B, const float* W, const float* b,
+                      int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W, const float* b,
                       float* slab, hipStream_t st);
 void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, double* metrics, int B,
                        int64_t* c0, int64_t* c1, hipStream_t st);
 void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, const float* W,
                      const float* b, double* metrics, hipStream_t st);
+
+// ---------------------------------------------------------------- data
+void launch_gather_epoch(const uint8_t* images, const int32_t* labels, const int32_t* idx, int n,
+                         uint8_t* out_images, int32_t* out_labels, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer
 constexpr int OPT_ADAM = 0;
@@ -52,7 +56,7 @@ void launch_optim(int kind, OptArgs& a, hipStream_t st);
 // ---------------------------------------------------------------- CNN (bf16)
 // Layouts (NHWC, see pytorch_distributed_mnist_amd/models/specs.py):
 //   x      uint8 [B][28*28]            gathered input bytes (for conv1 wgrad)
-//   a1     bf16  [B][26*26][32]        relu(conv1) output
+//   (a1 = relu(conv1) is never stored: the backward recomputes it from x)
 //   pool   bf16  [B][12*12][64]        maxpool(relu(conv2)) == fc1 input
 //   pmask  uint8 [B][12*12][64]        argmax in window (0..3) | 0x80 when > 0
 //   w2     bf16  [64][9][32]           conv2 weight (co, tap, ci)
@@ -67,9 +71,9 @@ constexpr int CNN_HEAD_SLAB = 1420;   // 1280 dWfc2 + 10 dbfc2 + 128 dbfc1 + los
 constexpr int CNN_CONV_SLAB = 18816;  // 18432 dW2 + 64 db2 + 288 dW1 + 32 db1
 
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                    const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
-                    const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, __bf16* a1,
-                    uint8_t* xg, int32_t* ylab, hipStream_t st);
+                    int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
+                    const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
+                    int32_t* ylab, hipStream_t st);
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st);
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
@@ -80,8 +84,13 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
                     hipStream_t st);
-void launch_cnn_bwd(const uint8_t* xg, const __bf16* a1, const __bf16* dpool, const uint8_t* pmask,
-                    const __bf16* w2t, int B, int imgs_per_block, float* slab, hipStream_t st);
+void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
+                    const uint8_t* pmask, const __bf16* w2t, int B, int imgs_per_block, float* slab,
+                    hipStream_t st);
 int cnn_bwd_blocks(int B, int imgs_per_block);
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st);
+
+// diagnostic timestamps (all zero unless built with PDM_STAMPS=1)
+void read_stamps_fwd(unsigned long long* host);
+void read_stamps_bwd(unsigned long long* host);

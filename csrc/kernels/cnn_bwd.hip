@@ -27,6 +27,7 @@ using namespace cnn;
 
 // ------------------------------------------------------------------ fc1_bwd
 constexpr int DW_TILES = FEAT / 64;  // 144
+constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
 
 __device__ __forceinline__ int tile_off(int row, int byte) {  // [32 rows][128 B], 2-way-free tr reads
   return row * 128 + (byte ^ (((row >> 3) & 1) << 5));
@@ -38,7 +39,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     bf16* __restrict__ dpool, const float* __restrict__ head_slab, int head_blocks,
     float* __restrict__ gwf2, float* __restrict__ gbf2, float* __restrict__ gbf1,
     double* __restrict__ metrics) {
-  __shared__ __attribute__((aligned(16))) char tile[32 * 128];
+  __shared__ __attribute__((aligned(16))) char tile[DWC * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
   const int nd = (ldt / 32) * DW_TILES;
@@ -46,6 +47,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 
   if (bid < DW_TILES) {
     // ---- dW1 tile: all 128 hidden rows x 64 feature columns, K = batch ----
+    // The batch is consumed in chunks of DWC rows: the whole chunk (pool rows and the
+    // dh^T A fragments) is loaded with every load in flight at once, and the next chunk's
+    // loads are issued before the current chunk's MFMAs.
     const int k0 = bid * 64;
     f32x4 acc[2][4];
 #pragma unroll
@@ -53,26 +57,52 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int srow = tid >> 3, sch = tid & 7;
-    for (int b0 = 0; b0 < ldt; b0 += 32) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (b0 + srow < B)
-        v = *reinterpret_cast<const uint4*>(pool + (int64_t)(b0 + srow) * FEAT + k0 + sch * 8);
-      __syncthreads();
-      *reinterpret_cast<uint4*>(tile + tile_off(srow, sch * 16)) = v;
-      __syncthreads();
-      bf16x8 a[2];
+    uint4 pv[DWC / 32];
+    bf16x8 a[2][DWC / 32];
+    auto load_chunk = [&](int c0) {
+#pragma unroll
+      for (int j = 0; j < DWC / 32; ++j) {
+        const int row = c0 + srow + 32 * j;
+        // clamped load + select: rows past B are zero (their dh rows are zero too, but
+        // stale pool memory could hold non-finite bit patterns)
+        const uint4 v = *reinterpret_cast<const uint4*>(pool + (int64_t)min(row, B - 1) * FEAT +
+                                                        k0 + sch * 8);
+        pv[j] = row < B ? v : make_uint4(0, 0, 0, 0);
+      }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
-        a[mt] = *reinterpret_cast<const bf16x8*>(dht + (int64_t)(wave * 32 + mt * 16 + i16) * ldt +
-                                                 b0 + 8 * g);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const s16x4 lo = lds_tr16(tile + tile_off(8 * g + q, 32 * nt + 8 * pq));
-        const s16x4 hi = lds_tr16(tile + tile_off(8 * g + 4 + q, 32 * nt + 8 * pq));
-        const bf16x8 bv = cat_tr(lo, hi);
+        for (int kk = 0; kk < DWC / 32; ++kk)
+          a[mt][kk] = *reinterpret_cast<const bf16x8*>(
+              dht + (int64_t)(wave * 32 + mt * 16 + i16) * ldt + min(c0 + 32 * kk, ldt - 32) + 8 * g);
+    };
+    load_chunk(0);
+    for (int c0 = 0; c0 < ldt; c0 += DWC) {
+      __syncthreads();   // previous chunk's tile reads are done
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], bv, acc[mt][nt], 0, 0, 0);
+      for (int j = 0; j < DWC / 32; ++j)
+        *reinterpret_cast<uint4*>(tile + tile_off(srow + 32 * j, sch * 16)) = pv[j];
+      bf16x8 ac[2][DWC / 32];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int kk = 0; kk < DWC / 32; ++kk) ac[mt][kk] = a[mt][kk];
+      __syncthreads();
+      if (c0 + DWC < ldt) load_chunk(c0 + DWC);
+      const int nk = min(DWC / 32, (ldt - c0) / 32);
+#pragma unroll
+      for (int kk = 0; kk < DWC / 32; ++kk) {
+        if (kk < nk) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const s16x4 lo = lds_tr16(tile + tile_off(32 * kk + 8 * g + q, 32 * nt + 8 * pq));
+            const s16x4 hi = lds_tr16(tile + tile_off(32 * kk + 8 * g + 4 + q, 32 * nt + 8 * pq));
+            const bf16x8 bv = cat_tr(lo, hi);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ac[mt][kk], bv, acc[mt][nt], 0, 0, 0);
+          }
+        }
       }
     }
 #pragma unroll
@@ -114,12 +144,29 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 
   // ---- head slab reduction (one block) ----
   for (int e = tid; e < HEAD_SLAB; e += 256) {
+    // 8 interleaved partial sums (8 loads in flight), combined in a fixed order
+    float sp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    double dp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int j = 0;
+    for (; j + 8 <= head_blocks; j += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float v = head_slab[(int64_t)(j + u) * HEAD_SLAB + e];
+        sp[u] += v;
+        dp[u] += (double)v;
+      }
+    }
+    for (int u = 0; j < head_blocks; ++j, ++u) {
+      const float v = head_slab[(int64_t)j * HEAD_SLAB + e];
+      sp[u] += v;
+      dp[u] += (double)v;
+    }
     float s = 0.f;
     double sd = 0.0;
-    for (int j = 0; j < head_blocks; ++j) {
-      const float v = head_slab[(int64_t)j * HEAD_SLAB + e];
-      s += v;
-      sd += (double)v;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s += sp[u];
+      sd += dp[u];
     }
     if (e < NCLS * HID) gwf2[e] = s;
     else if (e < NCLS * HID + NCLS) gbf2[e - NCLS * HID] = s;
@@ -131,127 +178,222 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 
 // ------------------------------------------------------------------ cnn_bwd
 constexpr int BWD_THREADS = 512;
-constexpr int B_XS = 0;                         // fp32 [784]            3136
-constexpr int B_A1 = 3136;                      // a1 image              43264
-constexpr int B_DZ = B_A1 + P1 * 64;            // dz2 image             73728
-constexpr int B_RED = B_DZ + P2 * 128;          // fp32 reduction scratch
+constexpr int DZW = 28;                         // dz2 image padded by 2 on every side
+constexpr int B_XS = 0;                         // bf16 x [784] + zero pad 1600
+constexpr int B_A1 = 1600;                      // a1 image              43264
+constexpr int B_DZ = B_A1 + P1 * 64;            // padded dz2 image      100352
+constexpr int B_RED = B_DZ + DZW * DZW * 128;   // fp32 reduction scratch
 constexpr int RED_DB2 = 0;                      // [8 waves][64]
-constexpr int RED_DW1 = RED_DB2 + 8 * C2;       // [4 waves][288]
-constexpr int RED_DB1 = RED_DW1 + 4 * C1 * 9;   // [4 waves][32]
-constexpr int RED_N = RED_DB1 + 4 * C1;         // 1792 floats
-constexpr int B_TOTAL = B_RED + RED_N * 4;      // 127296 B -> 1 workgroup / CU
+constexpr int RED_DW1 = RED_DB2 + 8 * C2;       // [4 waves][32 ci][16 taps] (tap 9 = bias)
+constexpr int RED_N = RED_DW1 + 4 * C1 * 16;    // 2560 floats
+constexpr int B_MK = B_RED + RED_N * 4;         // relu'(a1) bitmask: u32 [676] (bit = ci)
+constexpr int B_TOTAL = B_MK + P1 * 4;           // 158160 B -> 1 workgroup / CU
 constexpr int SL_DB2 = C2 * 9 * C1;             // 18432
 constexpr int SL_DW1 = SL_DB2 + C2;             // 18496
 constexpr int SL_DB1 = SL_DW1 + C1 * 9;         // 18784
 
-// Stage one image into LDS: x (fp32), a1 (swizzled), dz2 (expanded from the pooled
-// gradient and the argmax|positive mask), and accumulate the conv2 bias gradient.
+// dz2 padded image: pixel (r, c) in [0,28)^2 holds dz2[r-2][c-2] (0 on the border), 128 B,
+// 16-B chunk XOR (2r + c) & 7: dgrad row reads conflict-free, wgrad transposed reads 2-way.
+__device__ __forceinline__ int dzp_off(int r, int c, int byte) {
+  return (r * DZW + c) * 128 + ((((byte >> 4) ^ ((2 * r + c) & 7))) << 4) + (byte & 15);
+}
+
+// Stage one image into LDS: x (bf16, zero-padded), dz2 (expanded from the pooled gradient
+// and the argmax|positive mask), accumulate the conv2 bias gradient, then recompute
+// a1 = relu(conv1(x)) into its LDS image (cheaper than a 43 KB/image HBM round trip).
+// Every global load of the image is issued before the first LDS store.
 __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_t* __restrict__ xg,
-                                               const bf16* __restrict__ a1g,
                                                const bf16* __restrict__ dpool,
-                                               const uint8_t* __restrict__ pmask, float (&db2p)[8]) {
-  const int tid = threadIdx.x;
-  float* xs = reinterpret_cast<float*>(smem + B_XS);
+                                               const uint8_t* __restrict__ pmask,
+                                               const float* __restrict__ w1,
+                                               const float* __restrict__ b1, bool first,
+                                               float (&db2p)[8]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  bf16* xs = reinterpret_cast<bf16*>(smem + B_XS);
   char* a1s = smem + B_A1;
   char* dzs = smem + B_DZ;
-  if (tid < 196) {
-    const uint32_t w = reinterpret_cast<const uint32_t*>(xg + (int64_t)img * 784)[tid];
-    float4 v;
-    v.x = pdm_normalize(w & 0xff);
-    v.y = pdm_normalize((w >> 8) & 0xff);
-    v.z = pdm_normalize((w >> 16) & 0xff);
-    v.w = pdm_normalize(w >> 24);
-    reinterpret_cast<float4*>(xs)[tid] = v;
-  }
-  const uint4* a1v = reinterpret_cast<const uint4*>(a1g + (int64_t)img * P1 * C1);
-  for (int c = tid; c < P1 * 4; c += BWD_THREADS) {
-    const int pix = c >> 2, ch = c & 3;
-    const int row = pix / H1, col = pix - row * H1;
-    *reinterpret_cast<uint4*>(a1s + a1_off(row, col, ch * 16)) = a1v[c];
-  }
+  uint32_t xw = 0;
+  if (tid < 196) xw = reinterpret_cast<const uint32_t*>(xg + (int64_t)img * 784)[tid];
   const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT);
   const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT);
-  for (int it = tid; it < PP * 8; it += BWD_THREADS) {  // it & 7 == tid & 7 (fixed channel chunk)
-    const int pp = it >> 3, ch = it & 7;
-    const int py = pp / HP, px = pp - py * HP;
-    const uint4 d = dpv[it];
-    const uint2 mk = mkv[it];
-    const uint16_t dv[8] = {(uint16_t)(d.x & 0xffff), (uint16_t)(d.x >> 16), (uint16_t)(d.y & 0xffff),
-                            (uint16_t)(d.y >> 16),    (uint16_t)(d.z & 0xffff), (uint16_t)(d.z >> 16),
-                            (uint16_t)(d.w & 0xffff), (uint16_t)(d.w >> 16)};
-    const uint8_t mb[8] = {(uint8_t)(mk.x & 0xff), (uint8_t)((mk.x >> 8) & 0xff),
-                           (uint8_t)((mk.x >> 16) & 0xff), (uint8_t)(mk.x >> 24),
-                           (uint8_t)(mk.y & 0xff), (uint8_t)((mk.y >> 8) & 0xff),
-                           (uint8_t)((mk.y >> 16) & 0xff), (uint8_t)(mk.y >> 24)};
+  uint4 d[3];
+  uint2 mk[3];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (mb[j] & 0x80) db2p[j] += __builtin_bit_cast(float, (uint32_t)dv[j] << 16);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      uint32_t w[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t lo = ((mb[2 * j] & 0x83) == (0x80 | s)) ? dv[2 * j] : 0u;
-        const uint32_t hi = ((mb[2 * j + 1] & 0x83) == (0x80 | s)) ? dv[2 * j + 1] : 0u;
-        w[j] = lo | (hi << 16);
-      }
-      *reinterpret_cast<uint4*>(dzs + dz_off(2 * py + (s >> 1), 2 * px + (s & 1), ch * 16)) =
-          make_uint4(w[0], w[1], w[2], w[3]);
+  for (int k = 0; k < 3; ++k) {
+    const int it = tid + k * BWD_THREADS;
+    if (it < PP * 8) {
+      d[k] = dpv[it];
+      mk[k] = mkv[it];
     }
+  }
+  if (tid < 196) {
+    bf16x4 v = {to_bf16(pdm_normalize(xw & 0xff)), to_bf16(pdm_normalize((xw >> 8) & 0xff)),
+                to_bf16(pdm_normalize((xw >> 16) & 0xff)), to_bf16(pdm_normalize(xw >> 24))};
+    reinterpret_cast<bf16x4*>(xs)[tid] = v;
+  } else if (tid < 200) {
+    reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};
+  }
+  if (threadIdx.x == 0) PDM_STAMP_VAL(11, PDM_CLOCK());
+  if (!first) {
+    // the previous image's scattered values must be cleared: zero the interior
+    for (int i = tid; i < P2 * 8; i += BWD_THREADS) {
+      const int pix = i >> 3, r = pix / H2, c = pix - r * H2;
+      *reinterpret_cast<uint4*>(dzs + ((r + 2) * DZW + c + 2) * 128 + (i & 7) * 16) =
+          make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // scatter: each pooled gradient goes to its window's argmax pixel (if it was > 0);
+  // dz2 is zero everywhere else.  For window pos s = 2dy + dx the padded pixel is
+  // base + (dy*28 + dx) and its chunk swizzle (2r + c) & 7 is (b0 + s) & 7.
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int it = tid + k * BWD_THREADS;   // it & 7 == tid & 7: fixed channel chunk
+    if (it < PP * 8) {
+      const int pp = it >> 3, ch = it & 7;
+      const int py = pp / HP, px = pp - py * HP;
+      const int base = ((2 * py + 2) * DZW + 2 * px + 2) * 128;
+      const int b0 = 4 * py + 2 * px + 6;
+      const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+      const uint32_t mw[2] = {mk[k].x, mk[k].y};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t mb = (mw[j >> 2] >> (8 * (j & 3))) & 0xff;
+        const uint32_t dv = (dw[j >> 1] >> (16 * (j & 1))) & 0xffff;
+        // branch-free: a non-positive window writes 0 to its (already zero) argmax pixel
+        const uint32_t dm = (mb & 0x80) ? dv : 0u;
+        db2p[j] += __builtin_bit_cast(float, dm << 16);
+        const int sw = mb & 3;
+        const int off = base + (sw >> 1) * (DZW * 128) + (sw & 1) * 128 +
+                        ((ch ^ ((b0 + sw) & 7)) << 4) + 2 * j;
+        *reinterpret_cast<uint16_t*>(dzs + off) = (uint16_t)dm;
+      }
+    }
+  }
+  if (threadIdx.x == 0) PDM_STAMP_VAL(12, PDM_CLOCK());
+  // conv1 operands (loaded here rather than kept live across the role loops);
+  // unconditional clamped loads + selects: no per-load branch / wait
+  bf16x4 w1f[2];
+  int toff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int tap = 4 * g + j;
+    toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const float wv = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
+      w1f[mt][j] = to_bf16(tap < 9 ? wv : 0.f);
+    }
+  }
+  f32x4 b1v[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  __syncthreads();
+  // conv1 recompute: D[co][pixel] on mfma_f32_16x16x16_bf16 (same math as cnn_fwd)
+  for (int nt = wave; nt < (P1 + 15) / 16; nt += BWD_THREADS / 64) {
+    const int P = min(nt * 16 + i16, P1 - 1);
+    const int y = P / H1, x = P - y * H1;
+    const int xb = y * IMG + x;
+    bf16x4 bx;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bx[j] = xs[toff[j] == IMG * IMG ? IMG * IMG : xb + toff[j]];
+    uint32_t bits = 0;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx, b1v[mt], 0, 0, 0);
+      bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
+                  to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        bits |= (from_bf16(o[r]) > 0.f ? 1u : 0u) << (16 * mt + 4 * g + r);
+      if (nt * 16 + i16 < P1) *reinterpret_cast<bf16x4*>(a1s + a1_off(y, x, 32 * mt + 8 * g)) = o;
+    }
+    // relu' bitmask of the pixel: OR the 4 lane groups' channel bits
+    bits |= __shfl_xor(bits, 16, 64);
+    bits |= __shfl_xor(bits, 32, 64);
+    if (g == 0 && nt * 16 + i16 < P1) reinterpret_cast<uint32_t*>(smem + B_MK)[nt * 16 + i16] = bits;
   }
 }
 
 __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
-    const uint8_t* __restrict__ xg, const bf16* __restrict__ a1g, const bf16* __restrict__ dpool,
-    const uint8_t* __restrict__ pmask, const bf16* __restrict__ w2t, int B, int ipb,
-    float* __restrict__ slab) {
+    const uint8_t* __restrict__ xg, const float* __restrict__ w1, const float* __restrict__ b1,
+    const bf16* __restrict__ dpool, const uint8_t* __restrict__ pmask,
+    const bf16* __restrict__ w2t, int B, int ipb, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) char smem[B_TOTAL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
   float* red = reinterpret_cast<float*>(smem + B_RED);
-  const float* xs = reinterpret_cast<const float*>(smem + B_XS);
+  const bf16* xs = reinterpret_cast<const bf16*>(smem + B_XS);
   const char* a1s = smem + B_A1;
   const char* dzs = smem + B_DZ;
+  const uint32_t* mks = reinterpret_cast<const uint32_t*>(smem + B_MK);
   float* out = slab + (int64_t)blockIdx.x * CONV_SLAB;
   float db2p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  PDM_STAMP(0);
+
+  // zero the whole padded dz2 image once: the border is never written, the interior
+  // only receives the scattered pooled gradients (re-zeroed for every further image)
+  for (int i = tid; i < DZW * DZW * 8; i += BWD_THREADS)
+    *reinterpret_cast<uint4*>(smem + B_DZ + i * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
 
   if (wave < 4) {
     // ===== conv2 weight gradient: (tap, ci-tile) pairs {w, w+4, ...} x all 4 co tiles =====
+    // K = output pixels in chunks of 8 along a row (24 = 3 chunks): lane group g of k-step
+    // ks takes chunk 4ks+g; its lane q reads pixels x = col0+q and x+4 (col0 % 8 == 0), so
+    // every swizzle term below is a per-lane constant and each read costs one add.
     f32x4 acc[5][4];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool five = wave < 2;  // 18 pairs over 4 waves: 5,5,4,4
+    const bool five = wave < 2;  // 18 pairs over 4 waves: 5,5,4,4 (+1 discarded on 2,3)
+    int cpair[5];
+#pragma unroll
+    for (int pi = 0; pi < 5; ++pi) {
+      const int pair = min(wave + 4 * pi, 17);
+      const int tap = pair >> 1, nt = pair & 1;
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      cpair[pi] = (ky * H1 + kx) * 64 + (((2 * nt + (pq >> 1)) ^ ((q + kx) & 3)) << 4) + 8 * (pq & 1);
+    }
+    const int u8b = 8 * (pq & 1);
     for (int i = 0; i < ipb; ++i) {
       const int img = blockIdx.x * ipb + i;
-      if (img < B) bwd_load_image(smem, img, xg, a1g, dpool, pmask, db2p);
+      if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
       __syncthreads();
+      PDM_STAMP(1);
       if (img < B) {
+#pragma unroll 2
         for (int ks = 0; ks < P2 / 32; ++ks) {
-          const int pa = ks * 32 + 8 * g + q, pb = pa + 4;
-          const int ya = pa / H2, xa = pa - ya * H2, yb = pb / H2, xb = pb - yb * H2;
+          const int c8 = ks * 4 + g;
+          const int row = c8 / 3;
+          const int x = (c8 - 3 * row) * 8 + q;
+          const int abase = (row * H1 + x) * 64;
+          const int dbase = ((row + 2) * DZW + x + 2) * 128 + u8b;
+          const int t = (((pq >> 1) ^ ((2 * row + x + 6) & 7)) << 4);
           bf16x8 A[4];
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
-            A[mt] = cat_tr(lds_tr16(dzs + dz_off(ya, xa, mt * 32 + 8 * pq)),
-                           lds_tr16(dzs + dz_off(yb, xb, mt * 32 + 8 * pq)));
+            A[mt] = cat_tr(lds_tr16(dzs + dbase + ((32 * mt) ^ t)),
+                           lds_tr16(dzs + dbase + 512 + ((32 * mt) ^ t ^ 64)));
 #pragma unroll
-          for (int pi = 0; pi < 5; ++pi) {
-            if (pi == 4 && !five) break;
-            const int pair = wave + 4 * pi;
-            const int tap = pair >> 1, nt = pair & 1;
-            const int ky = tap / 3, kx = tap - ky * 3;
-            const bf16x8 Bv = cat_tr(lds_tr16(a1s + a1_off(ya + ky, xa + kx, nt * 32 + 8 * pq)),
-                                     lds_tr16(a1s + a1_off(yb + ky, xb + kx, nt * 32 + 8 * pq)));
+          for (int pi = 0; pi < 5; ++pi) {   // waves 2,3: pair 4 is a discarded duplicate
+            const bf16x8 Bv = cat_tr(lds_tr16(a1s + abase + cpair[pi]),
+                                     lds_tr16(a1s + abase + cpair[pi] + 256));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt)
               acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mt], Bv, acc[pi][mt], 0, 0, 0);
           }
         }
       }
+      PDM_STAMP(2);
       __syncthreads();
+      PDM_STAMP(3);
     }
     // dW2[co][tap][ci]: rows co = 16mt + 4g + r, col ci = 16nt + i16
 #pragma unroll
@@ -267,90 +409,134 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     }
   } else {
     // ===== conv2 input gradient + relu'(a1) + conv1 weight/bias gradient =====
+    // Loop order (tap, K-half) outer, m-tile inner: the wave's 11 m-tiles keep their
+    // accumulators in registers for the whole image while only the 2 W2^T fragments of
+    // the current (tap, K-half) are live (prefetched one step ahead from L2), so the LDS
+    // reads of A can be issued well ahead of their MFMAs.
     const int wd = wave - 4;
-    bf16x8 wt[9][2][2];  // B[k = co][n = ci] = W2^T[tap][ci][co]
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          wt[t][kh][nt] = *reinterpret_cast<const bf16x8*>(
-              w2t + (t * C1 + nt * 16 + i16) * C2 + 32 * kh + 8 * g);
-    float dw1p[2][9], db1p[2] = {0.f, 0.f};
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int t = 0; t < 9; ++t) dw1p[nt][t] = 0.f;
-    const bf16x8 zero8 = {};
+    constexpr int MTP = 6;                        // m-tiles per pass; 2 passes = 12 slots >= 11
+    // conv1 wgrad as a 16x16x16 MFMA: M = ci, N = tap (0..8; 9 = ones -> bias), K = pixels.
+    // The dgrad accumulator (lane: ci = i16, pixels 4g+r) is already its A operand.
+    const int ctap = i16;
+    const int cky = ctap / 3, ckx = ctap - 3 * cky;
+    const int xoff = (ctap < 9) ? (cky * IMG + ckx) : IMG * IMG;   // -> zero pad / ones
+    f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const bf16 one = to_bf16(1.f);
+    const bf16* w2l = w2t;
+    auto wfrag = [&](int t, int kh, int nt) {
+      return *reinterpret_cast<const bf16x8*>(w2l + (t * C1 + nt * 16 + i16) * C2 + 32 * kh + 8 * g);
+    };
+    unsigned long long t_mf = 0, t_ep = 0;
     for (int i = 0; i < ipb; ++i) {
       const int img = blockIdx.x * ipb + i;
-      if (img < B) bwd_load_image(smem, img, xg, a1g, dpool, pmask, db2p);
+      if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
       __syncthreads();
       if (img < B) {
-        for (int mt = wd; mt < (P1 + 15) / 16; mt += 4) {
-          const int P = mt * 16 + i16;
-          const int y = P / H1, x = P - y * H1;
-          const bool vP = P < P1;
-          f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 1
+        for (int pass = 0; pass < 2; ++pass) {
+          const unsigned long long c0 = PDM_CLOCK();
+          const int k0 = pass * MTP;
+          asm volatile("" : "+s"(w2l));   // opaque per pass: the W2^T loads must not be hoisted
+          // per-m-tile lane constants: padded-image pixel base and swizzle seed.  Slots past
+          // the wave's last real m-tile compute on clamped pixels and are discarded below.
+          int dbase[MTP], s0[MTP];
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
+          for (int k = 0; k < MTP; ++k) {
+            const int P = min((wd + 4 * (k0 + k)) * 16 + i16, P1 - 1);
+            const int y = P / H1, x = P - y * H1;
+            dbase[k] = ((y + 2) * DZW + x + 2) * 128;
+            s0[k] = 2 * y + x + 6;
+          }
+          f32x4 acc[MTP][2];
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-              const int oy = y - ky, ox = x - kx;
-              const bool v = vP && oy >= 0 && oy < H2 && ox >= 0 && ox < H2;
-              const int oyc = v ? oy : 0, oxc = v ? ox : 0;
+          for (int k = 0; k < MTP; ++k) acc[k][0] = acc[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          // straight-line (tap, K-half) steps; each W2^T fragment is loaded 4 steps ahead
+          // into its own register (no register rotation -> counted vmcnt waits)
+          bf16x8 w[18][2];
 #pragma unroll
-              for (int kh = 0; kh < 2; ++kh) {
-                bf16x8 a = *reinterpret_cast<const bf16x8*>(dzs + dz_off(oyc, oxc, (g + 4 * kh) * 16));
-                a = v ? a : zero8;
+          for (int tk = 0; tk < 4; ++tk) {
+            w[tk][0] = wfrag(tk >> 1, tk & 1, 0);
+            w[tk][1] = wfrag(tk >> 1, tk & 1, 1);
+          }
+          // A fragments (dz2 rows) are read one step ahead into a second register set
+          auto read_a = [&](int tk, bf16x8 (&a)[MTP]) {
+            const int t = tk >> 1, kh = tk & 1;
+            const int ky = t / 3, kx = t - 3 * ky;
+            const int toffb = (ky * DZW + kx) * 128;
+            const int gk = g + 4 * kh;
+            const int sk = 2 * ky + kx;
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
-                  acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wt[ky * 3 + kx][kh][nt],
-                                                                    acc[nt], 0, 0, 0);
-              }
+            for (int k = 0; k < MTP; ++k)
+              a[k] = *reinterpret_cast<const bf16x8*>(
+                  dzs + dbase[k] - toffb + ((gk ^ ((s0[k] - sk) & 7)) << 4));
+          };
+          bf16x8 a[2][MTP];
+          read_a(0, a[0]);
+#pragma unroll
+          for (int tk = 0; tk < 18; ++tk) {
+            __builtin_amdgcn_sched_barrier(0);   // keep each step's loads where they are issued
+            if (tk + 4 < 18) {
+              w[tk + 4][0] = wfrag((tk + 4) >> 1, (tk + 4) & 1, 0);
+              w[tk + 4][1] = wfrag((tk + 4) >> 1, (tk + 4) & 1, 1);
             }
-          // epilogue: lane holds pixels mt*16 + 4g + r, channel ci = 16nt + i16
+            if (tk + 1 < 18) read_a(tk + 1, a[(tk + 1) & 1]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int Pr = mt * 16 + 4 * g + r;
-            if (Pr < P1) {
-              const int yr = Pr / H1, xr = Pr - yr * H1;
-              float xv[9];
-#pragma unroll
-              for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) xv[ky * 3 + kx] = xs[(yr + ky) * IMG + xr + kx];
-#pragma unroll
-              for (int nt = 0; nt < 2; ++nt) {
-                const int ci = nt * 16 + i16;
-                const bf16 av = *reinterpret_cast<const bf16*>(a1s + a1_off(yr, xr, ci * 2));
-                const float dz1 = (from_bf16(av) > 0.f) ? acc[nt][r] : 0.f;
-                db1p[nt] += dz1;
-#pragma unroll
-                for (int t = 0; t < 9; ++t) dw1p[nt][t] = fmaf(dz1, xv[t], dw1p[nt][t]);
-              }
+            for (int k = 0; k < MTP; ++k) {
+              acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][0], acc[k][0], 0, 0, 0);
+              acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][1], acc[k][1], 0, 0, 0);
             }
           }
+          const unsigned long long c1 = PDM_CLOCK();
+          t_mf += c1 - c0;
+          // epilogue per m-tile: relu'(a1) mask -> dz1 (bf16) -> conv1 wgrad MFMA.  Lane holds
+          // pixels 16mt + 4g + r for channel ci = 16nt + i16.  Branch-free: invalid pixels
+          // read pixel 0 and are zeroed by select.
+#pragma unroll
+          for (int k = 0; k < MTP; ++k) {
+            {
+              const int P0 = (wd + 4 * (k0 + k)) * 16 + 4 * g;
+              const int y0 = P0 / H1, x0 = P0 - y0 * H1;
+              bf16x4 bx;
+              uint32_t mw[4];
+              bool valid[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const bool wrap = x0 + r >= H1;
+                const int yr = wrap ? y0 + 1 : y0, xr = wrap ? x0 + r - H1 : x0 + r;
+                valid[r] = P0 + r < P1;
+                const int yc = valid[r] ? yr : 0, xc = valid[r] ? xr : 0;
+                const int xi = (ctap < 9) ? yc * IMG + xc + xoff : IMG * IMG;
+                bx[r] = xs[xi];
+                mw[r] = mks[yc * H1 + xc];
+              }
+              if (ctap == 9) bx = bf16x4{one, one, one, one};
+              bf16x4 az[2];
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                  az[nt][r] = to_bf16((valid[r] && ((mw[r] >> (16 * nt + i16)) & 1u)) ? acc[k][nt][r] : 0.f);
+#pragma unroll
+              for (int nt = 0; nt < 2; ++nt)
+                acc1[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az[nt], bx, acc1[nt], 0, 0, 0);
+            }
+          }
+          t_ep += PDM_CLOCK() - c1;
         }
       }
       __syncthreads();
     }
-    // reduce over the 4 lanes sharing a channel (g = 0..3), then per-wave scratch
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      float v = db1p[nt];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (g == 0) red[RED_DB1 + wd * C1 + nt * 16 + i16] = v;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        float u = dw1p[nt][t];
-        u += __shfl_xor(u, 16, 64);
-        u += __shfl_xor(u, 32, 64);
-        if (g == 0) red[RED_DW1 + wd * C1 * 9 + (nt * 16 + i16) * 9 + t] = u;
-      }
+    if (tid == 256) {
+      PDM_STAMP_VAL(8, t_mf);
+      PDM_STAMP_VAL(9, t_ep);
+      PDM_STAMP_VAL(10, PDM_CLOCK());
     }
+    // acc1[nt]: rows ci = 16nt + 4g + r, col tap = i16
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[RED_DW1 + wd * C1 * 16 + (nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
   }
   // conv2 bias: lanes sharing (lane & 7) hold the same 8 channels
 #pragma unroll
@@ -362,20 +548,18 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     if (lane < 8) red[RED_DB2 + wave * C2 + lane * 8 + j] = v;
   }
   __syncthreads();
+  PDM_STAMP(4);
   if (tid < C2) {
     float s = 0.f;
     for (int w = 0; w < 8; ++w) s += red[RED_DB2 + w * C2 + tid];
     out[SL_DB2 + tid] = s;
-  } else if (tid >= 64 && tid < 64 + C1 * 9) {
-    const int e = tid - 64;
+  } else if (tid >= 64 && tid < 64 + C1 * 10) {
+    const int e = tid - 64;             // (ci, tap) with tap 0..8 = weight, 9 = bias
+    const int ci = e / 10, t = e - 10 * ci;
     float s = 0.f;
-    for (int w = 0; w < 4; ++w) s += red[RED_DW1 + w * C1 * 9 + e];
-    out[SL_DW1 + e] = s;
-  } else if (tid >= 384 && tid < 384 + C1) {
-    const int e = tid - 384;
-    float s = 0.f;
-    for (int w = 0; w < 4; ++w) s += red[RED_DB1 + w * C1 + e];
-    out[SL_DB1 + e] = s;
+    for (int w = 0; w < 4; ++w) s += red[RED_DW1 + w * C1 * 16 + ci * 16 + t];
+    if (t < 9) out[SL_DW1 + ci * 9 + t] = s;
+    else out[SL_DB1 + ci] = s;
   }
 }
 
@@ -417,13 +601,24 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
 
 int cnn_bwd_blocks(int B, int ipb) { return (B + ipb - 1) / ipb; }
 
-void launch_cnn_bwd(const uint8_t* xg, const __bf16* a1, const __bf16* dpool, const uint8_t* pmask,
-                    const __bf16* w2t, int B, int ipb, float* slab, hipStream_t st) {
-  cnn_bwd_kernel<<<cnn_bwd_blocks(B, ipb), BWD_THREADS, 0, st>>>(xg, a1, dpool, pmask, w2t, B, ipb,
-                                                                 slab);
+void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
+                    const uint8_t* pmask, const __bf16* w2t, int B, int ipb, float* slab,
+                    hipStream_t st) {
+  cnn_bwd_kernel<<<cnn_bwd_blocks(B, ipb), BWD_THREADS, 0, st>>>(xg, w1, b1, dpool, pmask, w2t, B,
+                                                                 ipb, slab);
 }
 
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st) {
   conv_reduce_kernel<<<(CONV_SLAB + 255) / 256, 256, 0, st>>>(slab, nblk, gw2, gb2, gw1, gb1);
 }
+
+#ifdef PDM_STAMPS
+void read_stamps_bwd(unsigned long long* host) {
+  hipMemcpyFromSymbol(host, HIP_SYMBOL(pdm_stamps), sizeof(unsigned long long) * 256 * 16);
+}
+#else
+void read_stamps_bwd(unsigned long long* host) {
+  for (int i = 0; i < 256 * 16; ++i) host[i] = 0;
+}
+#endif

@@ -3,6 +3,30 @@
 #include "../common.h"
 #include "../kernels.h"
 
+// Diagnostic build only (PDM_STAMPS=1 python -m pytorch_distributed_mnist_amd.build):
+// thread 0 of blocks 0..255 records s_memtime at phase boundaries; never in a timed build.
+#ifdef PDM_STAMPS
+static __device__ unsigned long long pdm_stamps[256 * 16];
+#define PDM_STAMP(slot)                                                              \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 256)                                        \
+      pdm_stamps[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memtime();           \
+  } while (0)
+#define PDM_CLOCK() __builtin_amdgcn_s_memtime()
+#define PDM_STAMP_VAL(slot, val)                                                     \
+  do {                                                                               \
+    if (blockIdx.x < 256) pdm_stamps[blockIdx.x * 16 + (slot)] = (val);              \
+  } while (0)
+#else
+#define PDM_STAMP(slot) \
+  do {                  \
+  } while (0)
+#define PDM_CLOCK() 0ull
+#define PDM_STAMP_VAL(slot, val) \
+  do {                           \
+  } while (0)
+#endif
+
 namespace cnn {
 
 constexpr int IMG = 28;               // input 28x28

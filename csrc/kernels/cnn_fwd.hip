@@ -22,140 +22,161 @@ namespace {
 using namespace cnn;
 
 // ---- cnn_fwd LDS carve (one static array; every offset 16-B aligned) ----
-constexpr int F_XS = 0;                       // fp32 [28*28]          3136 B
-constexpr int F_A1 = 3136;                    // bf16 a1 image         43264 B
-constexpr int F_PS = F_A1 + P1 * 64;          // bf16 pooled [144][64] 18432 B
-constexpr int F_MS = F_PS + PP * C2 * 2;      // u8 mask [144][64]     9216 B
-constexpr int F_TOTAL = F_MS + PP * C2;       // 74048 B -> 2 workgroups / CU
+constexpr int FWD_THREADS = 512;
+constexpr int F_XS = 0;                       // bf16 x [28*28] + zero pad  1600 B
+constexpr int F_A1 = 1600;                    // bf16 a1 image              43264 B
+constexpr int F_PS = F_A1 + P1 * 64;          // bf16 pooled [144][64]      18432 B
+constexpr int F_MS = F_PS + PP * C2 * 2;      // u8 mask [144][64]          9216 B
+constexpr int F_TOTAL = F_MS + PP * C2;       // 72512 B -> 2 workgroups / CU
 
 template <bool TRAIN>
-__global__ __launch_bounds__(256, 2) void cnn_fwd_kernel(
+__global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ idx, const int64_t* __restrict__ ctr, int bfull,
+    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
-    bf16* __restrict__ a1g, uint8_t* __restrict__ xg, int32_t* __restrict__ ylab) {
+    uint8_t* __restrict__ xg, int32_t* __restrict__ ylab) {
   __shared__ __attribute__((aligned(16))) char smem[F_TOTAL];
-  float* xs = reinterpret_cast<float*>(smem + F_XS);
+  bf16* xs = reinterpret_cast<bf16*>(smem + F_XS);
   char* a1s = smem + F_A1;
   bf16* ps = reinterpret_cast<bf16*>(smem + F_PS);
   uint8_t* ms = reinterpret_cast<uint8_t*>(smem + F_MS);
 
   const int img = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t src = idx ? (int64_t)idx[(*ctr) * (int64_t)bfull + img] : (int64_t)img;
-
-  // 1. gather + normalise (torchvision ToTensor/Normalize semantics)
-  if (tid < 196) {
-    const uint32_t w = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];
-    float4 v;
-    v.x = pdm_normalize(w & 0xff);
-    v.y = pdm_normalize((w >> 8) & 0xff);
-    v.z = pdm_normalize((w >> 16) & 0xff);
-    v.w = pdm_normalize(w >> 24);
-    reinterpret_cast<float4*>(xs)[tid] = v;
-    if (TRAIN) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[tid] = w;
-  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  PDM_STAMP(0);
+  // 1. gather: the dependent chain (counter -> index -> image row) is issued before
+  // anything else so its latency is not queued behind the weight loads.
+  // sample row: sampler index (idx), epoch-buffer row (ctr only) or plain row (eval)
+  // (clamped to the row space: a counter driven past the epoch reads a valid row)
+  const int64_t row = min(ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img, nrow - 1);
+  const int64_t src = idx ? (int64_t)idx[row] : row;
+  uint32_t xw = 0;
+  if (tid < 196) xw = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];
   if (tid == 0) ylab[img] = labels[src];
 
-  // conv1 weights for this thread's fixed channel group (8 channels)
-  const int cg = tid & 3;
-  f32x2 w1r[9][4];
-  f32x2 b1r[4];
+  // conv2 B fragments for this wave's two n-tiles (co = 32*(wave&1) + 16*j + i16):
+  // lane l holds B[k = ci = 8g + e][n = co] = w2[co][tap][ci]
+  const int nh = wave & 1;
+  bf16x8 wb[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      wb[t][j] = *reinterpret_cast<const bf16x8*>(
+          w2 + ((nh * 32 + j * 16 + i16) * 9 + t) * 32 + 8 * g);
+  // conv1 as D[co][pixel] = W1[co][tap] . X[tap][pixel] on mfma_f32_16x16x16_bf16:
+  // A = weights (lane row co = i16, k = taps 4g..4g+3, zero past tap 8), B = input
+  // patches (lane col = pixel, k = taps); bias is the initial accumulator.
+  bf16x4 w1f[2];
+  int toff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    b1r[j] = f32x2{b1[cg * 8 + 2 * j], b1[cg * 8 + 2 * j + 1]};
+    const int tap = 4 * g + j;
+    toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;  // -> zero pad entry
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
-      w1r[t][j] = f32x2{w1[(cg * 8 + 2 * j) * 9 + t], w1[(cg * 8 + 2 * j + 1) * 9 + t]};
-  }
-  __syncthreads();
-
-  // 2. conv1 + bias + ReLU (packed fp32 FMAs), -> LDS a1 image (+ global a1)
-  for (int it = tid; it < P1 * 4; it += 256) {
-    const int pix = it >> 2;
-    const int row = pix / H1, col = pix - row * H1;
-    f32x2 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = b1r[j];
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const float xv = xs[(row + ky) * IMG + col + kx];
-        const f32x2 xx = {xv, xv};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __builtin_elementwise_fma(xx, w1r[ky * 3 + kx][j], acc[j]);
-      }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[2 * j] = to_bf16(fmaxf(acc[j][0], 0.f));
-      o[2 * j + 1] = to_bf16(fmaxf(acc[j][1], 0.f));
+    for (int mt = 0; mt < 2; ++mt) {   // clamped unconditional load + select (no branch/wait)
+      const float wv = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
+      w1f[mt][j] = to_bf16(tap < 9 ? wv : 0.f);
     }
-    *reinterpret_cast<bf16x8*>(a1s + a1_off(row, col, cg * 16)) = o;
-    if (TRAIN) *reinterpret_cast<bf16x8*>(a1g + ((int64_t)img * P1 + pix) * C1 + cg * 8) = o;
   }
+  f32x4 b1v[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  float b2r[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b2r[j] = b2[nh * 32 + j * 16 + i16];
 
-  // conv2 B fragments, all 9 taps x 4 n-tiles, held in registers for the whole image:
-  // lane l holds B[k = ci = 8(l>>4)+j][n = co = 16nt + (l&15)] = w2[co][tap][ci]
-  bf16x8 wb[9][4];
-  {
-    const int co_l = lane & 15, ci0 = 8 * (lane >> 4);
+  if (tid < 196) {
+    bf16x4 v = {to_bf16(pdm_normalize(xw & 0xff)), to_bf16(pdm_normalize((xw >> 8) & 0xff)),
+                to_bf16(pdm_normalize((xw >> 16) & 0xff)), to_bf16(pdm_normalize(xw >> 24))};
+    reinterpret_cast<bf16x4*>(xs)[tid] = v;
+    if (TRAIN) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[tid] = xw;
+  } else if (tid < 200) {
+    reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};   // zero pad (taps 9..15)
+  }
+  __syncthreads();
+  PDM_STAMP(1);
+
+  // 2. conv1 + bias + ReLU -> LDS a1 image; lane holds 4 consecutive channels of one
+  // pixel -> one 8-byte LDS store per 16x16 tile
+  for (int nt = wave; nt < (P1 + 15) / 16; nt += FWD_THREADS / 64) {
+    const int P = min(nt * 16 + i16, P1 - 1);
+    const int y = P / H1, x = P - y * H1;
+    const int xb = y * IMG + x;
+    bf16x4 bx;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bx[j] = xs[toff[j] == IMG * IMG ? IMG * IMG : xb + toff[j]];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx, b1v[mt], 0, 0, 0);
+      bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
+                  to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
+      if (nt * 16 + i16 < P1)  // channels co = 16mt + 4g .. +3 = byte 32mt + 8g
+        *reinterpret_cast<bf16x4*>(a1s + a1_off(y, x, 32 * mt + 8 * g)) = o;
+    }
+  }
+  __syncthreads();
+  PDM_STAMP(2);
+
+  // 3. conv2 implicit GEMM: 36 tiles of 16 rows (4 pooled pixels x 2x2 window) x 64 co;
+  // wave w takes tiles (w>>1) + 4k for its two n-tiles.  Tile (py, px0) is wave-uniform
+  // and px0 % 4 == 0, so the A-read swizzle term ((ox + kx) & 3) = ((2q + (s&1) + kx) & 3)
+  // is a per-lane constant: the 9 per-tap lane offsets are precomputed.
+  const int q = i16 >> 2, s = i16 & 3;
+  const int lp = ((s >> 1) * H1 + 2 * q + (s & 1)) * 64;
+  int aoff[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+      aoff[ky * 3 + kx] = lp + (ky * H1 + kx) * 64 + ((g ^ ((2 * q + (s & 1) + kx) & 3)) << 4);
+  for (int tt = wave >> 1; tt < 36; tt += FWD_THREADS / 128) {
+    const int py = tt / 3, px0 = 4 * (tt - py * 3);
+    const char* tb = a1s + (2 * py * H1 + 2 * px0) * 64;
+    bf16x8 a[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) a[t] = *reinterpret_cast<const bf16x8*>(tb + aoff[t]);
+    f32x4 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = f32x4{b2r[j], b2r[j], b2r[j], b2r[j]};
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        wb[t][nt] = *reinterpret_cast<const bf16x8*>(w2 + ((nt * 16 + co_l) * 9 + t) * 32 + ci0);
-  }
-  float b2r[4];
+      for (int j = 0; j < 2; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], wb[t][j], acc[j], 0, 0, 0);
+    // epilogue: lane holds the 2x2 window (4 regs) of pooled pixel pp for channel co
+    const int pp = py * HP + px0 + g;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) b2r[nt] = b2[nt * 16 + (lane & 15)];
-  __syncthreads();
-
-  // 3. conv2 implicit GEMM: 36 tiles of 16 rows (4 pooled pixels x 2x2 window) x 64 co
-  const int m = lane & 15, q = m >> 2, s = m & 3;
-  const int chb = (lane >> 4) * 16;
-  for (int tt = wave; tt < 36; tt += 4) {
-    const int py = tt / 3, px0 = 4 * (tt - py * 3);
-    const int oy = 2 * py + (s >> 1), ox = 2 * (px0 + q) + (s & 1);
-    f32x4 acc[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(a1s + a1_off(oy + ky, ox + kx, chb));
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[ky * 3 + kx][nt], acc[nt], 0, 0, 0);
-      }
-    // epilogue: lane holds window (4 regs) of pooled pixel pp for channel co
-    const int pp = py * HP + px0 + (lane >> 4);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int co = nt * 16 + (lane & 15);
-      float best = fmaxf(acc[nt][0] + b2r[nt], 0.f);
+    for (int j = 0; j < 2; ++j) {
+      const int co = nh * 32 + j * 16 + i16;
+      float best = fmaxf(acc[j][0], 0.f);
       int bi = 0;
 #pragma unroll
       for (int r = 1; r < 4; ++r) {
-        const float v = fmaxf(acc[nt][r] + b2r[nt], 0.f);
+        const float v = fmaxf(acc[j][r], 0.f);
         if (v > best) { best = v; bi = r; }          // first max in (dy, dx) row-major order
       }
       ps[pp * C2 + co] = to_bf16(best);
       ms[pp * C2 + co] = (uint8_t)(bi | (best > 0.f ? 0x80 : 0));
     }
   }
+  PDM_STAMP(3);
   __syncthreads();
+  PDM_STAMP(4);
 
   // 4. coalesced write-out of pooled activations + mask
   uint4* pout = reinterpret_cast<uint4*>(pool + (int64_t)img * FEAT);
-  for (int i = tid; i < FEAT * 2 / 16; i += 256) pout[i] = reinterpret_cast<const uint4*>(ps)[i];
+  for (int i = tid; i < FEAT * 2 / 16; i += FWD_THREADS) pout[i] = reinterpret_cast<const uint4*>(ps)[i];
   if (TRAIN) {
     uint4* mout = reinterpret_cast<uint4*>(pmask + (int64_t)img * FEAT);
-    for (int i = tid; i < FEAT / 16; i += 256) mout[i] = reinterpret_cast<const uint4*>(ms)[i];
+    for (int i = tid; i < FEAT / 16; i += FWD_THREADS) mout[i] = reinterpret_cast<const uint4*>(ms)[i];
   }
+  PDM_STAMP(5);
 }
 
 // ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
@@ -329,15 +350,15 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
 }  // namespace
 
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                    const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
-                    const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, __bf16* a1,
-                    uint8_t* xg, int32_t* ylab, hipStream_t st) {
-  if (a1 != nullptr)
-    cnn_fwd_kernel<true><<<B, 256, 0, st>>>(images, labels, idx, ctr, bfull, w1, b1, w2, b2, pool,
-                                            pmask, a1, xg, ylab);
+                    int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
+                    const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
+                    int32_t* ylab, hipStream_t st) {
+  if (xg != nullptr)
+    cnn_fwd_kernel<true><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1, w2,
+                                                    b2, pool, pmask, xg, ylab);
   else
-    cnn_fwd_kernel<false><<<B, 256, 0, st>>>(images, labels, idx, ctr, bfull, w1, b1, w2, b2,
-                                             pool, pmask, a1, xg, ylab);
+    cnn_fwd_kernel<false><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1, w2,
+                                                     b2, pool, pmask, xg, ylab);
 }
 
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
@@ -359,3 +380,13 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
                                                  ldt, slab, metrics, c0, c1);
   }
 }
+
+#ifdef PDM_STAMPS
+void read_stamps_fwd(unsigned long long* host) {
+  hipMemcpyFromSymbol(host, HIP_SYMBOL(pdm_stamps), sizeof(unsigned long long) * 256 * 16);
+}
+#else
+void read_stamps_fwd(unsigned long long* host) {
+  for (int i = 0; i < 256 * 16; ++i) host[i] = 0;
+}
+#endif

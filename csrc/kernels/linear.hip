@@ -24,12 +24,14 @@ constexpr int WPR = K / 4;      // 196 uint32 words per image
 // nrows are zero.
 __device__ __forceinline__ void load_rows(float (*xs)[K], const uint8_t* images, const int32_t* idx,
                                           int64_t base, int row0, int nrows, int rows_cap,
-                                          bool gather) {
+                                          bool gather, int64_t nrow = 0) {
   for (int i = threadIdx.x; i < rows_cap * WPR; i += blockDim.x) {
     const int r = i / WPR, w = i - r * WPR;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (r < nrows) {
-      const int64_t s = gather ? (int64_t)idx[base + row0 + r] : (int64_t)(row0 + r);
+      // gather rows are clamped to the index buffer: a counter driven past the epoch
+      // (misuse) reads a valid row instead of faulting
+      const int64_t s = gather ? (int64_t)idx[min(base + row0 + r, nrow - 1)] : (int64_t)(row0 + r);
       const uint32_t word = reinterpret_cast<const uint32_t*>(images + s * K)[w];
       v.x = pdm_normalize(word & 0xff);
       v.y = pdm_normalize((word >> 8) & 0xff);
@@ -81,15 +83,15 @@ __device__ __forceinline__ float row_xent(const float (&lg)[N], int y, float (&p
 
 __global__ __launch_bounds__(256) void lin_train_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ idx, const int64_t* __restrict__ ctr, int bfull, int B,
-    const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ slab) {
+    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
+    int B, const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ slab) {
   __shared__ float xs[ROWS][K];
   __shared__ float dl[ROWS][N];
   __shared__ float red[ROWS][2];
   const int row0 = blockIdx.x * ROWS;
   const int nrows = min(ROWS, B - row0);
   const int64_t base = (*ctr) * (int64_t)bfull;
-  load_rows(xs, images, idx, base, row0, nrows, ROWS, true);
+  load_rows(xs, images, idx, base, row0, nrows, ROWS, true, nrow);
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
     row_logits(xs[r], W, bias, lg);
     if (lane == 0) {
       if (r < nrows) {
-        const int y = labels[idx[base + row0 + r]];
+        const int y = labels[idx[min(base + row0 + r, nrow - 1)]];
         int correct;
         const float loss = row_xent(lg, y, p, correct);
 #pragma unroll
@@ -193,10 +195,10 @@ __global__ __launch_bounds__(256) void lin_eval_kernel(
 }  // namespace
 
 void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                      const int64_t* ctr, int bfull, int B, const float* W, const float* b,
-                      float* slab, hipStream_t st) {
+                      int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W,
+                      const float* b, float* slab, hipStream_t st) {
   const int nblk = (B + ROWS - 1) / ROWS;
-  lin_train_kernel<<<nblk, 256, 0, st>>>(images, labels, idx, ctr, bfull, B, W, b, slab);
+  lin_train_kernel<<<nblk, 256, 0, st>>>(images, labels, idx, nrow, ctr, bfull, B, W, b, slab);
 }
 
 void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, double* metrics, int B,

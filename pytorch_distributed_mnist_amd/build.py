@@ -64,6 +64,8 @@ def compile_flags(abi: int, inc):
     flags += [f"-I{p}" for p in inc]
     if os.environ.get("PDM_DEBUG_BOUNDS"):
         flags.append("-DPDM_DEBUG_BOUNDS=1")
+    if os.environ.get("PDM_STAMPS"):
+        flags.append("-DPDM_STAMPS=1")
     return flags
 
 
@@ -76,7 +78,8 @@ def _hash(path, flags, hdr_digest):
     return h.hexdigest()[:20]
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
+          out: str | None = None) -> str:
     inc, lib, abi, _ = _torch_paths()
     flags = compile_flags(abi, inc)
     os.makedirs(OBJ_DIR, exist_ok=True)
@@ -114,7 +117,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     objs = [o for o, _ in results]
 
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    out = os.path.join(PKG, "_C" + suffix)
+    out = out or os.path.join(PKG, "_C" + suffix)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     link = ([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs +
             [f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
              "-ltorch_hip", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{lib}"])
@@ -126,7 +130,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     os.replace(out + ".tmp", out)
     # drop stale objects of sources that no longer exist / older hashes
     keep = set(objs)
-    for o in glob.glob(os.path.join(OBJ_DIR, "*.o")):
+    for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not os.environ.get("PDM_STAMPS") else []:
         if o not in keep:
             try:
                 os.unlink(o)
@@ -140,8 +144,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--out", default=None, help="output .so path (default: in-tree _C*.so)")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, out=a.out)
     print(f"built {out}")
 
 

@@ -23,6 +23,9 @@ _ERR = None
 
 
 def ext_path():
+    override = os.environ.get("PDM_EXT_PATH")   # diagnostic builds (e.g. PDM_STAMPS)
+    if override:
+        return override
     cands = sorted(glob.glob(os.path.join(_PKG_DIR, "_C*.so")))
     return cands[0] if cands else None
 

@@ -3,13 +3,13 @@
 Kernel chain of one training step (all on the compute stream; the two bucket
 all-reduces fork onto the RCCL stream):
 
-  cnn_fwd      gather+normalise, conv1+ReLU, conv2+ReLU+maxpool  -> pool, mask, a1, x
+  cnn_fwd      gather+normalise, conv1+ReLU, conv2+ReLU+maxpool  -> pool, mask, x
   fc1_fwd      split-K fc1 GEMM                                  -> fp32 partials
   cnn_head     fc1 reduce+bias+ReLU, fc2, CE, head backward      -> dh, dh^T, head slabs
                (advances the data-step and optimizer-step counters)
   fc1_bwd      dW1 tiles | dX tiles | head-slab reduce           -> bucket 0 complete
   [all-reduce bucket 0 on the comm stream, overlapping the next two kernels]
-  cnn_bwd      conv2 wgrad | conv2 dgrad + conv1 wgrad           -> conv slabs
+  cnn_bwd      a1 recompute, conv2 wgrad | conv2 dgrad + conv1 wgrad -> conv slabs
   conv_reduce  fixed-order slab sum                              -> bucket 1 complete
   [all-reduce bucket 1]
   optim        SGD/Adam over the arena + bf16 weight copies (W1, W1^T, W2, W2^T)
@@ -52,7 +52,6 @@ class CnnStep(GpuStepBase):
         # activations / workspaces (sized once; graphs capture their addresses)
         self.pool = torch.empty(cap * 9216, dtype=bf16, device=dev)
         self.pmask = torch.empty(cap * 9216, dtype=torch.uint8, device=dev)
-        self.a1 = torch.empty(B * 676 * 32, dtype=bf16, device=dev)
         self.xg = torch.empty(B * 784, dtype=torch.uint8, device=dev)
         self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
         self.splitk_train = choose_splitk(B)
@@ -79,7 +78,20 @@ class CnnStep(GpuStepBase):
                                     "fc2.weight", "fc2.bias")}
         self.G = {n: g(n) for n in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias",
                                     "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")}
+        self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
         self.refresh_shadows()
+
+    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
+        """Upload the epoch order, then materialise the epoch's samples contiguously."""
+        n = idx_cpu.numel()
+        if self.ep_images.numel() != n * 784:
+            self.ep_images = torch.empty(n * 784, dtype=torch.uint8, device=self.device)
+            self.ep_labels = torch.empty(n, dtype=torch.int32, device=self.device)
+            self.graphs.clear()
+        super().set_train_indices(idx_cpu)
+        self.C.gather_epoch(self.train_images, self.train_labels, self.idx,
+                            self.ep_images.view(n, 784), self.ep_labels)
 
     @torch.no_grad()
     def refresh_shadows(self) -> None:
@@ -108,9 +120,9 @@ class CnnStep(GpuStepBase):
         C, P, G = self.C, self.P, self.G
         ldt = -(-B // 32) * 32
         S = self.splitk_train
-        C.cnn_fwd(self.train_images, self.train_labels, self.idx, self.ctr[0:1], self.bfull, B,
+        C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                  self.pmask, self.a1, self.xg, self.ylab)
+                  self.pmask, self.xg, self.ylab)
         C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
         C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab, True,
                    self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
@@ -120,7 +132,8 @@ class CnnStep(GpuStepBase):
                   self.metrics.train_view())
         self.reducer.bucket_ready(0)
         ipb = choose_ipb(B)
-        C.cnn_bwd(self.xg, self.a1, self.dpool, self.pmask, self.w2t, B, ipb, self.conv_slab)
+        C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
+                  ipb, self.conv_slab)
         C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
         self.reducer.bucket_ready(1)
@@ -135,7 +148,7 @@ class CnnStep(GpuStepBase):
             b = min(EVAL_CHUNK, n - s)
             C.cnn_fwd(self.test_images[s:s + b], self.test_labels[s:s + b], None, None, b, b,
                       P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                      self.pmask, None, None, self.ylab)
+                      self.pmask, None, self.ylab)
             C.fc1_fwd(self.pool, self.wf1, self.part, b, S)
             C.cnn_head(self.part, S, b, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
                        False, None, None, 32, None, self.metrics.eval_view(), None, None)

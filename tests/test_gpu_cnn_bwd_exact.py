@@ -22,7 +22,13 @@ def test_cnn_bwd_exact(gpu, B, ipb):
     C = _C()
     g = torch.Generator().manual_seed(B)
     xg = torch.randint(0, 256, (B, 784), generator=g, dtype=torch.uint8)
-    a1 = torch.relu(torch.randn(B, 676, 32, generator=g)).to(torch.bfloat16)
+    w1 = torch.randn(32, 9, generator=g) * 0.3
+    b1 = torch.randn(32, generator=g) * 0.1
+    xn = ((xg.to(torch.float32) / 255.0 - 0.1307) / 0.3081).to(torch.bfloat16).float()
+    # the kernel recomputes a1 = bf16(relu(conv1(bf16 x, bf16 w1) + b1))
+    a1 = torch.relu(torch.nn.functional.conv2d(
+        xn.view(B, 1, 28, 28), w1.to(torch.bfloat16).float().view(32, 1, 3, 3), b1))
+    a1 = a1.permute(0, 2, 3, 1).reshape(B, 676, 32).to(torch.bfloat16)
     dpool = torch.randn(B, 9216, generator=g).to(torch.bfloat16)
     s = torch.randint(0, 4, (B, 9216), generator=g)
     pos = torch.rand(B, 9216, generator=g) < 0.7
@@ -31,7 +37,8 @@ def test_cnn_bwd_exact(gpu, B, ipb):
     w2t = w2.reshape(64, 288).t().contiguous()                             # [tap*32+ci][co]
     nblk = C.cnn_bwd_nblk(B, ipb)
     slab = torch.zeros(nblk * C.CNN_CONV_SLAB, device=gpu)
-    C.cnn_bwd(xg.to(gpu), a1.to(gpu), dpool.to(gpu), pmask.to(gpu), w2t.to(gpu), B, ipb, slab)
+    C.cnn_bwd(xg.to(gpu), w1.to(gpu), b1.to(gpu), dpool.to(gpu), pmask.to(gpu), w2t.to(gpu), B,
+              ipb, slab)
     gw2 = torch.zeros(64 * 288, device=gpu)
     gb2 = torch.zeros(64, device=gpu)
     gw1 = torch.zeros(288, device=gpu)
@@ -54,15 +61,18 @@ def test_cnn_bwd_exact(gpu, B, ipb):
     ref_gb2 = dzn.sum((0, 2, 3))
     da1 = torch.nn.grad.conv2d_input(a1n.shape, W2, dzn)
     dz1 = da1 * (a1n > 0)
-    x = ((xg.to(torch.float32) / 255.0 - 0.1307) / 0.3081).to(d).view(B, 1, 28, 28)
+    # conv1 wgrad runs on a bf16 MFMA: dz1 and x enter it rounded to bf16
+    dz1 = dz1.to(torch.bfloat16).to(d)
+    x = ((xg.to(torch.float32) / 255.0 - 0.1307) / 0.3081).to(torch.bfloat16).to(d)
+    x = x.view(B, 1, 28, 28)
     ref_gw1 = torch.nn.grad.conv2d_weight(x, (32, 1, 3, 3), dz1)
     ref_gb1 = dz1.sum((0, 2, 3))
 
     got_gw2 = gw2.cpu().double().view(64, 3, 3, 32).permute(0, 3, 1, 2)
-    assert rel(got_gw2, ref_gw2) < 1e-5
+    assert rel(got_gw2, ref_gw2) < 1e-4     # a1 recompute may round a few values differently
     assert rel(gb2.cpu().double(), ref_gb2) < 1e-5
-    assert rel(gw1.cpu().double().view(32, 1, 3, 3), ref_gw1) < 1e-5
-    assert rel(gb1.cpu().double(), ref_gb1) < 1e-5
+    assert rel(gw1.cpu().double().view(32, 1, 3, 3), ref_gw1) < 1e-4
+    assert rel(gb1.cpu().double(), ref_gb1) < 1e-4
 
 
 @pytest.mark.parametrize("B", [64, 40, 1])

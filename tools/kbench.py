@@ -1,0 +1,65 @@
+"""Per-kernel timing of the CNN step kernels at several batch sizes (CUDA events)."""
+import sys
+import torch
+sys.path.insert(0, ".")
+from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+from pytorch_distributed_mnist_amd.runtime.program import build_local_program
+from pytorch_distributed_mnist_amd.runtime.cnn_step import choose_ipb
+
+train = synthetic_split(60000, True)
+test = synthetic_split(512, False)
+
+
+def timeit(fn, iters=50):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+for B in [int(b) for b in (sys.argv[1:] or ["256", "1024", "4096"])]:
+    p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.01,
+                            use_graphs=False)
+    p.optimizer.sync_hyperparams()
+    p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+    st = p.gpu
+    C, P, G = st.C, st.P, st.G
+    ldt = -(-B // 32) * 32
+    S = st.splitk_train
+    ipb = choose_ipb(B)
+    st.train_step(B)
+    torch.cuda.synchronize()
+    z = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ks = {
+        "cnn_fwd": lambda: C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, z, B, B,
+                                     P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"],
+                                     st.pool, st.pmask, st.xg, st.ylab),
+        "fc1_fwd": lambda: C.fc1_fwd(st.pool, st.wf1, st.part, B, S),
+        "cnn_head": lambda: C.cnn_head(st.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
+                                       st.ylab, True, st.dh, st.dht, ldt, st.head_slab,
+                                       st.metrics.train_view(), None, None),
+        "fc1_bwd": lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"],
+                                     st.dpool, st.head_slab, G["fc2.weight"], G["fc2.bias"],
+                                     G["fc1.bias"], st.metrics.train_view()),
+        "cnn_bwd": lambda: C.cnn_bwd(st.xg, P["conv1.weight"], P["conv1.bias"], st.dpool, st.pmask,
+                                     st.w2t, B, ipb, st.conv_slab),
+        "conv_reduce": lambda: C.conv_reduce(st.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"],
+                                             G["conv2.bias"], G["conv1.weight"], G["conv1.bias"]),
+        "optim": lambda: st.launch_optimizer(),
+    }
+    tot = 0.0
+    line = []
+    for name, fn in ks.items():
+        us = timeit(fn)
+        tot += us
+        line.append(f"{name}={us:.1f}")
+    st.ctr.zero_()   # each step advances the data counter: stay inside the epoch buffer
+    step = timeit(lambda: st._train_impl(B), max(1, min(20, len(train) // B - 2)))
+    print(f"B={B:5d} S={S} ipb={ipb} " + " ".join(line) + f" | sum={tot:.1f}us step={step:.1f}us "
+          f"-> {B / step * 1e6 / 1e6:.2f}M img/s", flush=True)
