@@ -252,7 +252,7 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
 void fc1_fwd(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_t splitk) {
   c10::DeviceGuard g(pool.device());
   TORCH_CHECK(B >= 1, "B must be >= 1");
-  TORCH_CHECK(splitk >= 1 && (CNN_FEAT / 32) % splitk == 0, "splitk must divide 288");
+  TORCH_CHECK(splitk >= 1 && 32 % splitk == 0, "splitk must divide 32");
   need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
   need_min(wf1, at::kBFloat16, (int64_t)CNN_HID * CNN_FEAT, "wf1");
   need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
@@ -340,6 +340,8 @@ void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, 
                  at::Tensor gb1) {
   c10::DeviceGuard g(slab.device());
   need_min(slab, at::kFloat, nblk * CNN_CONV_SLAB, "conv slab");
+  need_aligned(slab.data_ptr(), 16, "conv slab");
+  TORCH_CHECK(nblk >= 1, "nblk must be >= 1");
   need(gw2, at::kFloat, "gw2");
   need(gb2, at::kFloat, "gb2");
   need(gw1, at::kFloat, "gw1");

@@ -564,28 +564,49 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
 }
 
 // ------------------------------------------------------------------ conv_reduce
+constexpr int CR_COLS = 64;     // slab columns per conv_reduce workgroup (294 workgroups)
+static_assert(CONV_SLAB % CR_COLS == 0, "conv slab must split into whole column tiles");
+
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restrict__ slab, int nblk,
                                                           float* __restrict__ gw2,
                                                           float* __restrict__ gb2,
                                                           float* __restrict__ gw1,
                                                           float* __restrict__ gb1) {
-  // block = 256 consecutive slab columns; each thread sums every slab for 1 column with
-  // 8 independent accumulators (8 loads in flight), fixed order -> deterministic.
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= CONV_SLAB) return;
-  const float* p = slab + e;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int j = 0;
-  for (; j + 8 <= nblk; j += 8) {
+  // workgroup = 64 slab columns x 16 slab groups: lane c4 = tid & 15 owns 4 columns (float4),
+  // group rg = tid >> 4 sums slabs rg, rg + 16, ... in batches of 8 loads in flight; the 16
+  // group sums are combined in a fixed order -> deterministic.
+  __shared__ float4 red[16][CR_COLS / 4];
+  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
+  const int col = blockIdx.x * CR_COLS + 4 * c4;
+  const float4* p = reinterpret_cast<const float4*>(slab + col);
+  constexpr int STRIDE4 = CONV_SLAB / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j0 = rg; j0 < nblk; j0 += 16 * 8) {
+    float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += p[(int64_t)(j + u) * CONV_SLAB];
+    for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)min(j0 + 16 * u, nblk - 1) * STRIDE4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool on = j0 + 16 * u < nblk;
+      acc.x += on ? v[u].x : 0.f;
+      acc.y += on ? v[u].y : 0.f;
+      acc.z += on ? v[u].z : 0.f;
+      acc.w += on ? v[u].w : 0.f;
+    }
   }
-  for (; j < nblk; ++j) acc[0] += p[(int64_t)j * CONV_SLAB];
-  const float t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  if (e < SL_DB2) gw2[e] = t;
-  else if (e < SL_DW1) gb2[e - SL_DB2] = t;
-  else if (e < SL_DB1) gw1[e - SL_DW1] = t;
-  else gb1[e - SL_DB1] = t;
+  red[rg][c4] = acc;
+  __syncthreads();
+  if (tid < CR_COLS) {
+    const float* rf = reinterpret_cast<const float*>(&red[0][0]);
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += rf[g * CR_COLS + tid];
+    const int e = blockIdx.x * CR_COLS + tid;
+    if (e < SL_DB2) gw2[e] = t;
+    else if (e < SL_DW1) gb2[e - SL_DB2] = t;
+    else if (e < SL_DB1) gw1[e - SL_DW1] = t;
+    else gb1[e - SL_DB1] = t;
+  }
 }
 
 }  // namespace
@@ -610,7 +631,7 @@ void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const _
 
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st) {
-  conv_reduce_kernel<<<(CONV_SLAB + 255) / 256, 256, 0, st>>>(slab, nblk, gw2, gb2, gw1, gb1);
+  conv_reduce_kernel<<<CONV_SLAB / CR_COLS, 256, 0, st>>>(slab, nblk, gw2, gb2, gw1, gb1);
 }
 
 #ifdef PDM_STAMPS

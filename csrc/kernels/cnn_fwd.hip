@@ -180,6 +180,8 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 }
 
 // ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
+constexpr int FC1_KB = 9;   // k-steps per load batch (288 k-steps = 32 batches)
+
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
                                                       float* __restrict__ part, int B, int kchunk) {
@@ -199,16 +201,24 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 3
-  for (int k = 0; k < kchunk; k += 32) {
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(pa0 + k);
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(pa1 + k);
-    const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(pb0 + k);
-    const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(pb1 + k);
-    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, w0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, w1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, w0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, w1, acc[1][1], 0, 0, 0);
+  // K in batches of FC1_KB steps: every operand load of a batch is issued before its
+  // MFMAs (kchunk is a multiple of 32 * FC1_KB: split factors divide 32)
+  for (int kb = 0; kb < kchunk; kb += 32 * FC1_KB) {
+    bf16x8 a0[FC1_KB], a1[FC1_KB], w0[FC1_KB], w1[FC1_KB];
+#pragma unroll
+    for (int i = 0; i < FC1_KB; ++i) {
+      a0[i] = *reinterpret_cast<const bf16x8*>(pa0 + kb + 32 * i);
+      a1[i] = *reinterpret_cast<const bf16x8*>(pa1 + kb + 32 * i);
+      w0[i] = *reinterpret_cast<const bf16x8*>(pb0 + kb + 32 * i);
+      w1[i] = *reinterpret_cast<const bf16x8*>(pb1 + kb + 32 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < FC1_KB; ++i) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w0[i], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w1[i], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w0[i], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w1[i], acc[1][1], 0, 0, 0);
+    }
   }
   float* out = part + (int64_t)sidx * B * HID;
 #pragma unroll
@@ -244,12 +254,27 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
     h[0] = ba.x; h[1] = ba.y; h[2] = ba.z; h[3] = ba.w;
     h[4] = bb.x; h[5] = bb.y; h[6] = bb.z; h[7] = bb.w;
   }
-  if (valid) {
-    for (int s = 0; s < S; ++s) {
-      const float4* p = reinterpret_cast<const float4*>(part + ((int64_t)s * B + row) * HID + 8 * j);
-      const float4 u = p[0], v = p[1];
-      h[0] += u.x; h[1] += u.y; h[2] += u.z; h[3] += u.w;
-      h[4] += v.x; h[5] += v.y; h[6] += v.z; h[7] += v.w;
+  {
+    // split-K partials in batches of 8 (16 loads in flight; clamped addresses + selects,
+    // so no per-load branch), summed in split order
+    const int rc = min(row, B - 1);
+    for (int s0 = 0; s0 < S; s0 += 8) {
+      float4 u[8], v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4* p = reinterpret_cast<const float4*>(
+            part + ((int64_t)min(s0 + q, S - 1) * B + rc) * HID + 8 * j);
+        u[q] = p[0];
+        v[q] = p[1];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const bool on = s0 + q < S;
+        h[0] += on ? u[q].x : 0.f; h[1] += on ? u[q].y : 0.f;
+        h[2] += on ? u[q].z : 0.f; h[3] += on ? u[q].w : 0.f;
+        h[4] += on ? v[q].x : 0.f; h[5] += on ? v[q].y : 0.f;
+        h[6] += on ? v[q].z : 0.f; h[7] += on ? v[q].w : 0.f;
+      }
     }
   }
 #pragma unroll

@@ -26,11 +26,12 @@ from .gpu_step import GpuStepBase
 EVAL_CHUNK = 2048
 
 
-def choose_splitk(B: int, cap: int = 16, target_blocks: int = 256) -> int:
-    """Split-K factor for fc1_fwd: a divisor of 288 (K-steps of 32) giving ~target blocks."""
+def choose_splitk(B: int, cap: int = 32, target_blocks: int = 256) -> int:
+    """Split-K factor for fc1_fwd: a divisor of 32 (so every split holds whole 9-step load
+    batches of the 288 K-steps) giving ~target_blocks workgroups."""
     mtiles = (B + 31) // 32
     best = 1
-    for s in (1, 2, 3, 4, 6, 8, 9, 12, 16, 18, 24, 32):
+    for s in (1, 2, 4, 8, 16, 32):
         if s <= cap and mtiles * s <= target_blocks:
             best = s
     return best
