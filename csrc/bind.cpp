@@ -282,7 +282,8 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
     TORCH_CHECK(dh && dht && slab, "train mode needs dh, dht, slab");
     need_min(*dh, at::kBFloat16, ldt * CNN_HID, "dh");
     need_min(*dht, at::kBFloat16, ldt * CNN_HID, "dht");
-    need_min(*slab, at::kFloat, (ldt / CNN_HEAD_ROWS) * CNN_HEAD_SLAB, "head slab");
+    need_min(*slab, at::kFloat, (int64_t)cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)) * CNN_HEAD_SLAB,
+             "head slab");
     pdh = ptr<__bf16>(*dh);
     pdht = ptr<__bf16>(*dht);
     pslab = slab->data_ptr<float>();
@@ -309,7 +310,7 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
   need(gbf1, at::kFloat, "gbf1");
   TORCH_CHECK(gwf1.numel() == (int64_t)CNN_HID * CNN_FEAT && gwf2.numel() == CNN_NCLS * CNN_HID &&
                   gbf2.numel() == CNN_NCLS && gbf1.numel() == CNN_HID, "fc grad views");
-  const int64_t hb = ldt / CNN_HEAD_ROWS;
+  const int64_t hb = cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS));
   need_min(head_slab, at::kFloat, hb * CNN_HEAD_SLAB, "head slab");
   need(metrics, at::kDouble, "metrics");
   need_numel(metrics, 3, "metrics");
@@ -377,6 +378,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("optim_step", &optim_step);
   m.def("gather_epoch", &gather_epoch);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
+  m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });
   m.attr("CNN_HEAD_SLAB") = CNN_HEAD_SLAB;
   m.attr("CNN_CONV_SLAB") = CNN_CONV_SLAB;
   m.def("cnn_fwd", &cnn_fwd);

@@ -66,7 +66,9 @@ void launch_optim(int kind, OptArgs& a, hipStream_t st);
 constexpr int CNN_FEAT = 9216;
 constexpr int CNN_HID = 128;
 constexpr int CNN_NCLS = 10;
-constexpr int CNN_HEAD_ROWS = 16;
+constexpr int CNN_HEAD_ROWS = 4;         // rows per head row group (one wave per row)
+constexpr int CNN_HEAD_MAX_BLOCKS = 256;  // head workgroups (grid-stride over row groups)
+int cnn_head_blocks(int groups);          // head workgroups = head slabs for `groups` row groups
 constexpr int CNN_HEAD_SLAB = 1420;   // 1280 dWfc2 + 10 dbfc2 + 128 dbfc1 + loss + correct
 constexpr int CNN_CONV_SLAB = 18816;  // 18432 dW2 + 64 db2 + 288 dW1 + 32 db1
 

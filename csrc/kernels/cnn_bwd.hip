@@ -28,6 +28,7 @@ using namespace cnn;
 // ------------------------------------------------------------------ fc1_bwd
 constexpr int DW_TILES = FEAT / 64;  // 144
 constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
+constexpr int HR_BLOCKS = (HEAD_SLAB + 63) / 64;   // head-slab reduction workgroups (23)
 
 __device__ __forceinline__ int tile_off(int row, int byte) {  // [32 rows][128 B], 2-way-free tr reads
   return row * 128 + (byte ^ (((row >> 3) & 1) << 5));
@@ -142,37 +143,38 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     return;
   }
 
-  // ---- head slab reduction (one block) ----
-  for (int e = tid; e < HEAD_SLAB; e += 256) {
-    // 8 interleaved partial sums (8 loads in flight), combined in a fixed order
-    float sp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    double dp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    int j = 0;
-    for (; j + 8 <= head_blocks; j += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float v = head_slab[(int64_t)(j + u) * HEAD_SLAB + e];
-        sp[u] += v;
-        dp[u] += (double)v;
-      }
-    }
-    for (int u = 0; j < head_blocks; ++j, ++u) {
-      const float v = head_slab[(int64_t)j * HEAD_SLAB + e];
-      sp[u] += v;
-      dp[u] += (double)v;
-    }
+  // ---- head slab reduction: HR_BLOCKS workgroups x 64 slab columns x 4 slab groups ----
+  {
+    __shared__ float rs[4][64];
+    __shared__ double rd[4][64];
+    const int e = (bid - DW_TILES - nd) * 64 + (tid & 63), grp = tid >> 6;
+    const int ec = min(e, HEAD_SLAB - 1);
     float s = 0.f;
     double sd = 0.0;
+    for (int j0 = grp; j0 < head_blocks; j0 += 4 * 8) {
+      float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      s += sp[u];
-      sd += dp[u];
+      for (int u = 0; u < 8; ++u)
+        v[u] = head_slab[(int64_t)min(j0 + 4 * u, head_blocks - 1) * HEAD_SLAB + ec];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float x = (j0 + 4 * u < head_blocks) ? v[u] : 0.f;
+        s += x;
+        sd += (double)x;
+      }
     }
-    if (e < NCLS * HID) gwf2[e] = s;
-    else if (e < NCLS * HID + NCLS) gbf2[e - NCLS * HID] = s;
-    else if (e < NCLS * HID + NCLS + HID) gbf1[e - NCLS * HID - NCLS] = s;
-    else if (e == HEAD_SLAB - 2) { metrics[0] += sd; metrics[2] += (double)B; }
-    else metrics[1] += sd;
+    rs[grp][tid & 63] = s;
+    rd[grp][tid & 63] = sd;
+    __syncthreads();
+    if (tid < 64 && e < HEAD_SLAB) {
+      s = ((rs[0][tid] + rs[1][tid]) + rs[2][tid]) + rs[3][tid];
+      sd = ((rd[0][tid] + rd[1][tid]) + rd[2][tid]) + rd[3][tid];
+      if (e < NCLS * HID) gwf2[e] = s;
+      else if (e < NCLS * HID + NCLS) gbf2[e - NCLS * HID] = s;
+      else if (e < NCLS * HID + NCLS + HID) gbf1[e - NCLS * HID - NCLS] = s;
+      else if (e == HEAD_SLAB - 2) { metrics[0] += sd; metrics[2] += (double)B; }
+      else metrics[1] += sd;
+    }
   }
 }
 
@@ -615,7 +617,7 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
                     hipStream_t st) {
-  const int nblk = DW_TILES + (ldt / 32) * DW_TILES + 1;
+  const int nblk = DW_TILES + (ldt / 32) * DW_TILES + HR_BLOCKS;
   fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, dht, ldt, pool, wf1t, B, gwf1, dpool, head_slab,
                                        head_blocks, gwf2, gbf2, gbf1, metrics);
 }

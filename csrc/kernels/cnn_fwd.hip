@@ -234,141 +234,135 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
 }
 
 // ---- head: fc1 reduce + bias + ReLU, fc2, CE, and (train) the head backward ----
+// One wave per batch row (HEAD_ROWS = 4 rows per workgroup, B/4 workgroups): lane j owns
+// hidden units 2j, 2j+1, so the fc2 logits are plain wave reductions and the split-K
+// partial loads of a row are spread over a whole wave.
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void cnn_head_kernel(
     const float* __restrict__ part, int S, int B, const float* __restrict__ bf1,
     const float* __restrict__ wf2, const float* __restrict__ bf2, const int32_t* __restrict__ ylab,
     bf16* __restrict__ dh, bf16* __restrict__ dht, int ldt, float* __restrict__ slab,
     double* __restrict__ metrics, int64_t* c0, int64_t* c1) {
+  static_assert(HEAD_ROWS == 4, "one wave per row, 4 waves");
   __shared__ float hs[HEAD_ROWS][HID];
   __shared__ float dhs[HEAD_ROWS][HID];
   __shared__ float dls[HEAD_ROWS][NCLS];
   __shared__ float red[HEAD_ROWS][2];
-  const int tid = threadIdx.x, r = tid >> 4, j = tid & 15;
-  const int row = blockIdx.x * HEAD_ROWS + r;
-  const bool valid = row < B;
-  float h[8];
-  {
-    const float4 ba = reinterpret_cast<const float4*>(bf1 + 8 * j)[0];
-    const float4 bb = reinterpret_cast<const float4*>(bf1 + 8 * j)[1];
-    h[0] = ba.x; h[1] = ba.y; h[2] = ba.z; h[3] = ba.w;
-    h[4] = bb.x; h[5] = bb.y; h[6] = bb.z; h[7] = bb.w;
-  }
-  {
-    // split-K partials in batches of 8 (16 loads in flight; clamped addresses + selects,
-    // so no per-load branch), summed in split order
-    const int rc = min(row, B - 1);
-    for (int s0 = 0; s0 < S; s0 += 8) {
-      float4 u[8], v[8];
+  const int tid = threadIdx.x, r = tid >> 6, j = tid & 63;
+  const int ngroups = (TRAIN ? ldt : B + HEAD_ROWS - 1) / HEAD_ROWS;
+  // per-thread slab accumulators across this workgroup's row groups (train)
+  float sw[5] = {0.f, 0.f, 0.f, 0.f, 0.f};   // dWfc2 entries tid + 256k
+  float sx = 0.f;                             // dbfc2 / dbfc1 / loss / correct entry
+  double el = 0.0, ec = 0.0;                  // eval metrics (thread 0)
+  int en = 0;
+  const float2 bias = reinterpret_cast<const float2*>(bf1)[j];
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int row = grp * HEAD_ROWS + r;
+    const bool valid = row < B;
+    float2 h = bias;
+    {
+      // split-K partials in batches of 16 loads in flight (clamped addresses + selects),
+      // summed in split order
+      const int rc = min(row, B - 1);
+      for (int s0 = 0; s0 < S; s0 += 16) {
+        float2 u[16];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float4* p = reinterpret_cast<const float4*>(
-            part + ((int64_t)min(s0 + q, S - 1) * B + rc) * HID + 8 * j);
-        u[q] = p[0];
-        v[q] = p[1];
-      }
+        for (int q = 0; q < 16; ++q)
+          u[q] = reinterpret_cast<const float2*>(
+              part + ((int64_t)min(s0 + q, S - 1) * B + rc) * HID)[j];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const bool on = s0 + q < S;
-        h[0] += on ? u[q].x : 0.f; h[1] += on ? u[q].y : 0.f;
-        h[2] += on ? u[q].z : 0.f; h[3] += on ? u[q].w : 0.f;
-        h[4] += on ? v[q].x : 0.f; h[5] += on ? v[q].y : 0.f;
-        h[6] += on ? v[q].z : 0.f; h[7] += on ? v[q].w : 0.f;
+        for (int q = 0; q < 16; ++q) {
+          const bool on = s0 + q < S;
+          h.x += on ? u[q].x : 0.f;
+          h.y += on ? u[q].y : 0.f;
+        }
       }
     }
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) h[i] = valid ? fmaxf(h[i], 0.f) : 0.f;
+    h.x = valid ? fmaxf(h.x, 0.f) : 0.f;
+    h.y = valid ? fmaxf(h.y, 0.f) : 0.f;
 
-  float lg[NCLS];
+    float lg[NCLS];
 #pragma unroll
-  for (int c = 0; c < NCLS; ++c) {
-    const float4 wa = reinterpret_cast<const float4*>(wf2 + c * HID + 8 * j)[0];
-    const float4 wb = reinterpret_cast<const float4*>(wf2 + c * HID + 8 * j)[1];
-    float p = h[0] * wa.x;
-    p = fmaf(h[1], wa.y, p); p = fmaf(h[2], wa.z, p); p = fmaf(h[3], wa.w, p);
-    p = fmaf(h[4], wb.x, p); p = fmaf(h[5], wb.y, p); p = fmaf(h[6], wb.z, p);
-    p = fmaf(h[7], wb.w, p);
-    lg[c] = group_sum<16>(p) + bf2[c];
-  }
-  const int y = valid ? ylab[row] : 0;
-  float prob[NCLS];
-  int correct;
-  const float loss = row_xent<NCLS>(lg, y, prob, correct);
-
-  if (!TRAIN) {
+    for (int c = 0; c < NCLS; ++c) {
+      const float2 w = reinterpret_cast<const float2*>(wf2 + c * HID)[j];
+      lg[c] = wave_sum(fmaf(h.y, w.y, h.x * w.x)) + bf2[c];
+    }
+    const int y = valid ? ylab[row] : 0;
+    float prob[NCLS];
+    int correct;
+    const float loss = row_xent<NCLS>(lg, y, prob, correct);
     if (j == 0) {
       red[r][0] = valid ? loss : 0.f;
       red[r][1] = valid ? (float)correct : 0.f;
     }
-    __syncthreads();
-    if (tid == 0) {
-      double l = 0.0, c = 0.0;
-      int n = 0;
-      for (int i = 0; i < HEAD_ROWS; ++i) {
-        l += red[i][0];
-        c += red[i][1];
-        n += (blockIdx.x * HEAD_ROWS + i < B);
+
+    if (TRAIN) {
+      const float invB = 1.f / (float)B;
+      float dl[NCLS];
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) dl[c] = valid ? (prob[c] - (c == y ? 1.f : 0.f)) * invB : 0.f;
+      float2 dhv = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) {
+        const float2 w = reinterpret_cast<const float2*>(wf2 + c * HID)[j];
+        dhv.x = fmaf(dl[c], w.x, dhv.x);
+        dhv.y = fmaf(dl[c], w.y, dhv.y);
       }
-      atomicAdd(&metrics[0], l);
-      atomicAdd(&metrics[1], c);
-      atomicAdd(&metrics[2], (double)n);
+      dhv.x = h.x > 0.f ? dhv.x : 0.f;
+      dhv.y = h.y > 0.f ? dhv.y : 0.f;
+      // row < ldt always: rows >= B write zeros (GEMM padding)
+      const bf16x2 o = {to_bf16(dhv.x), to_bf16(dhv.y)};
+      dht[(int64_t)(2 * j) * ldt + row] = o[0];
+      dht[(int64_t)(2 * j + 1) * ldt + row] = o[1];
+      *reinterpret_cast<bf16x2*>(dh + (int64_t)row * HID + 2 * j) = o;
+      reinterpret_cast<float2*>(hs[r])[j] = h;
+      reinterpret_cast<float2*>(dhs[r])[j] = dhv;
+      if (j == 0) {
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) dls[r][c] = dl[c];
+      }
+    }
+    __syncthreads();
+    if (TRAIN) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int e = tid + 256 * k;
+        const int c = e / HID, n = e - c * HID;
+        float a = sw[k];
+#pragma unroll
+        for (int i = 0; i < HEAD_ROWS; ++i) a = fmaf(dls[i][c], hs[i][n], a);
+        sw[k] = a;
+      }
+      if (tid < NCLS) {
+        for (int i = 0; i < HEAD_ROWS; ++i) sx += dls[i][tid];
+      } else if (tid >= 16 && tid < 16 + HID) {
+        for (int i = 0; i < HEAD_ROWS; ++i) sx += dhs[i][tid - 16];
+      } else if (tid == 254 || tid == 255) {
+        for (int i = 0; i < HEAD_ROWS; ++i) sx += red[i][tid - 254];
+      }
+    } else if (tid == 0) {
+      for (int i = 0; i < HEAD_ROWS; ++i) {
+        el += red[i][0];
+        ec += red[i][1];
+        en += (grp * HEAD_ROWS + i < B);
+      }
+    }
+    __syncthreads();   // LDS is rewritten by the next row group
+  }
+  if (!TRAIN) {
+    if (tid == 0) {
+      atomicAdd(&metrics[0], el);
+      atomicAdd(&metrics[1], ec);
+      atomicAdd(&metrics[2], (double)en);
     }
     return;
   }
-
-  const float invB = 1.f / (float)B;
-  float dl[NCLS];
-#pragma unroll
-  for (int c = 0; c < NCLS; ++c) dl[c] = valid ? (prob[c] - (c == y ? 1.f : 0.f)) * invB : 0.f;
-  float dhv[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    float a = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCLS; ++c) a = fmaf(dl[c], wf2[c * HID + 8 * j + i], a);
-    dhv[i] = (h[i] > 0.f) ? a : 0.f;
-  }
-  // row < ldt always (grid = ldt / 16): rows >= B write zeros (GEMM padding)
-  bf16x8 o;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    o[i] = to_bf16(dhv[i]);
-    dht[(int64_t)(8 * j + i) * ldt + row] = o[i];
-    hs[r][8 * j + i] = h[i];
-    dhs[r][8 * j + i] = dhv[i];
-  }
-  *reinterpret_cast<bf16x8*>(dh + (int64_t)row * HID + 8 * j) = o;
-  if (j == 0) {
-#pragma unroll
-    for (int c = 0; c < NCLS; ++c) dls[r][c] = dl[c];
-    red[r][0] = valid ? loss : 0.f;
-    red[r][1] = valid ? (float)correct : 0.f;
-  }
-  __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * HEAD_SLAB;
-  for (int e = tid; e < NCLS * HID; e += 256) {
-    const int c = e / HID, n = e - c * HID;
-    float a = 0.f;
 #pragma unroll
-    for (int i = 0; i < HEAD_ROWS; ++i) a = fmaf(dls[i][c], hs[i][n], a);
-    out[e] = a;
-  }
-  if (tid < NCLS) {
-    float a = 0.f;
-    for (int i = 0; i < HEAD_ROWS; ++i) a += dls[i][tid];
-    out[NCLS * HID + tid] = a;
-  } else if (tid >= 16 && tid < 16 + HID) {
-    const int n = tid - 16;
-    float a = 0.f;
-    for (int i = 0; i < HEAD_ROWS; ++i) a += dhs[i][n];
-    out[NCLS * HID + NCLS + n] = a;
-  } else if (tid == 255) {
-    float l = 0.f, c = 0.f;
-    for (int i = 0; i < HEAD_ROWS; ++i) { l += red[i][0]; c += red[i][1]; }
-    out[HEAD_SLAB - 2] = l;
-    out[HEAD_SLAB - 1] = c;
-  }
+  for (int k = 0; k < 5; ++k) out[tid + 256 * k] = sw[k];
+  if (tid < NCLS) out[NCLS * HID + tid] = sx;
+  else if (tid >= 16 && tid < 16 + HID) out[NCLS * HID + NCLS + tid - 16] = sx;
+  else if (tid == 254 || tid == 255) out[HEAD_SLAB - 2 + (tid - 254)] = sx;
   pdm_bump_counters(c0, c1);
 }
 
@@ -396,15 +390,17 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
                      hipStream_t st) {
-  if (train) {
-    cnn_head_kernel<true><<<ldt / HEAD_ROWS, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh,
-                                                           dht, ldt, slab, metrics, c0, c1);
-  } else {
-    const int nblk = (B + HEAD_ROWS - 1) / HEAD_ROWS;
+  const int groups = (train ? ldt : B + HEAD_ROWS - 1) / HEAD_ROWS;
+  const int nblk = cnn_head_blocks(groups);
+  if (train)
+    cnn_head_kernel<true><<<nblk, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh, dht, ldt,
+                                                slab, metrics, c0, c1);
+  else
     cnn_head_kernel<false><<<nblk, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh, dht,
                                                  ldt, slab, metrics, c0, c1);
-  }
 }
+
+int cnn_head_blocks(int groups) { return groups < CNN_HEAD_MAX_BLOCKS ? groups : CNN_HEAD_MAX_BLOCKS; }
 
 #ifdef PDM_STAMPS
 void read_stamps_fwd(unsigned long long* host) {

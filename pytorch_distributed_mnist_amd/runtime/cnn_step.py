@@ -61,7 +61,7 @@ class CnnStep(GpuStepBase):
         self.part = torch.empty(part_n, dtype=torch.float32, device=dev)
         self.dh = torch.zeros(self.ldt * 128, dtype=bf16, device=dev)
         self.dht = torch.zeros(self.ldt * 128, dtype=bf16, device=dev)
-        self.head_slab = torch.empty((self.ldt // 16) * C.CNN_HEAD_SLAB, dtype=torch.float32,
+        self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=torch.float32,
                                      device=dev)
         self.dpool = torch.empty(B * 9216, dtype=bf16, device=dev)
         self.ipb = choose_ipb(B)

@@ -86,7 +86,7 @@ def test_fc1_bwd_exact(gpu, B):
     dht = dh.t().contiguous()
     pool = torch.randn(B, 9216, generator=g).to(torch.bfloat16)
     w1 = torch.randn(128, 9216, generator=g).to(torch.bfloat16)
-    hb = ldt // 16
+    hb = C.cnn_head_nblk(ldt)
     head_slab = torch.randn(hb, C.CNN_HEAD_SLAB, generator=g)
     gwf1 = torch.zeros(128 * 9216, device=gpu)
     dpool = torch.zeros(B * 9216, dtype=torch.bfloat16, device=gpu)
