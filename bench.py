@@ -28,6 +28,13 @@ import time
 
 import torch
 
+# The number to beat (BASELINE.md protocol): the reference's own training loop with the CNN
+# swapped in, PyTorch eager + DDP/RCCL on one MI355X (tools/reference_eager.py, DataLoader with
+# 4 workers, fp32, SGD momentum, batch 256; profiles/reference_eager_n1.jsonl).  For N GPUs
+# the baseline is taken as N x this value, i.e. perfect weak scaling of the reference.
+REFERENCE_CNN_IMG_S_1GPU = 135369.5
+REFERENCE_LINEAR_IMG_S_1GPU = 221060.4
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -137,7 +144,9 @@ def main():
             if model == "cnn" else "images/sec (whole node) MNIST Linear DDP",
             "value": round(value, 1), "unit": "images/sec", "n_gpus": ws, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+            "scaling": "weak", "vs_baseline": round(value / (ws * (
+                REFERENCE_CNN_IMG_S_1GPU if model == "cnn" else REFERENCE_LINEAR_IMG_S_1GPU)), 3),
+            "dtype": dtype,
             "data": "synthetic (60k x 1x28x28 uint8, MNIST-shaped), random-init weights",
             "config": {"model": "mnist_cnn" if model == "cnn" else "mnist_linear",
                        "global_batch": global_batch, "batch_per_rank": B, "seq_len": None,
