@@ -61,6 +61,15 @@ def build_rank_state(args, rank: int, world_size: int, local_rank: int, init_pg:
     if "MASTER_ADDR" in os.environ and getattr(args, "_launched", False) and \
             not getattr(args, "_init_method_explicit", False):
         init_method = "env://"
+    elif getattr(args, "_launched", False) and init_method.startswith("tcp://") and \
+            os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
+        # torchrun workers connect to the agent's store as clients for ANY tcp:// init
+        # method; an explicit -i naming another endpoint must be hosted by rank 0 instead
+        # (the reference's launch-mode semantics), or every rank would wait for a server.
+        hostport = init_method[len("tcp://"):].split("?")[0]
+        master = "{}:{}".format(os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))
+        if hostport != master:
+            os.environ["TORCHELASTIC_USE_AGENT_STORE"] = "False"
     ctx = parallel.init_distributed(args.backend, init_method, world_size, rank, local_rank, device,
                                     timeout_s=args.timeout, init_pg=init_pg)
     return ctx

@@ -90,3 +90,35 @@ def test_cnn_sgd_cpu_two_ranks(tmp_path):
     sd = torch.load(tmp_path / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)
     assert list(sd["state_dict"])[0] == "module.conv1.weight"
     assert set(sd["optimizer"]["state"][0]) == {"momentum_buffer"}
+
+
+def run_torchrun(args, cwd, nproc=2, timeout=300):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "multi_proc_single_gpu.py"), "--device", "cpu", "--backend", "gloo",
+           "--synthetic"] + args
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("explicit_init", [False, True])
+def test_launch_mode_matches_spawn(tmp_path, explicit_init):
+    """torchrun (launch mode, reference S:278-281 / RM:8-35) gives the same run as spawn."""
+    d1, d2 = tmp_path / "spawn", tmp_path / "launch"
+    d1.mkdir()
+    d2.mkdir()
+    common = ["--epochs", "1", "--synthetic-size", "2048", "--seed", "4", "--world-size", "2"]
+    a = run_cli(common, d1)
+    extra = ["-i", f"tcp://127.0.0.1:{free_port()}"] if explicit_init else []
+    b = run_torchrun(common + extra, d2)
+    ea = sorted(l for l in a.splitlines() if l.startswith(("Epoch:", "rank:")))
+    eb = sorted(l for l in b.splitlines() if l.startswith(("Epoch:", "rank:")))
+    assert len(ea) == 4 and ea == eb, (ea, eb)
+    sa = torch.load(d1 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)["state_dict"]
+    sb = torch.load(d2 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)["state_dict"]
+    for k in sa:   # torchrun sets OMP_NUM_THREADS=1: CPU GEMM sums may differ in the last ulp
+        assert torch.allclose(sa[k], sb[k], atol=1e-6, rtol=0), k
