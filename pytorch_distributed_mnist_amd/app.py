@@ -44,6 +44,13 @@ def _printer(rank, prefix):
     return p
 
 
+def resolve_dtype(dtype: str, arch: str, device: torch.device) -> str:
+    """--dtype auto: bf16 for the CNN on GPU (its HIP kernels), fp32 otherwise."""
+    if dtype != "auto":
+        return dtype
+    return "bf16" if (arch == "cnn" and device.type == "cuda") else "fp32"
+
+
 def _seed_everything(seed: int) -> None:
     random.seed(seed)
     torch.manual_seed(seed)
@@ -123,7 +130,8 @@ def run(args):
                              synthetic_size=args.synthetic_size)
     test_split = load_split(args.root, False, synthetic=args.synthetic)
     reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds())
-    program = TrainProgram(args.arch, args.dtype, arena, optimizer, reducer, train_split, test_split,
+    dtype = resolve_dtype(args.dtype, args.arch, device)
+    program = TrainProgram(args.arch, dtype, arena, optimizer, reducer, train_split, test_split,
                            args.batch_size, use_graphs=args.graphs)
     trainer = Trainer(program)
 

@@ -61,8 +61,10 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument('--arch', choices=['linear', 'cnn'], default='linear',
                    help="linear = reference Net (Linear 784->10); cnn = north-star CNN")
     g.add_argument('--optimizer', choices=['adam', 'sgd'], default='adam')
-    g.add_argument('--dtype', choices=['fp32', 'bf16'], default='fp32',
-                   help='compute dtype of activations / GEMM inputs (master weights stay fp32)')
+    g.add_argument('--dtype', choices=['auto', 'fp32', 'bf16'], default='auto',
+                   help='compute dtype of activations / GEMM inputs (master weights stay fp32); '
+                        'auto = bf16 for the CNN on GPU, fp32 otherwise (the reference Linear '
+                        'model and every CPU run)')
     g.add_argument('--synthetic', action='store_true',
                    help='use deterministic synthetic MNIST-shaped data even if MNIST is on disk')
     g.add_argument('--synthetic-size', type=int, default=None,

@@ -71,6 +71,14 @@ class FlatOptimizer:
     def sync_step(self) -> None:
         self._step_dev.fill_(self.step_count)
 
+    def _check_kind(self, sd: dict) -> None:
+        """Refuse a torch optimizer state_dict written by the other optimizer kind."""
+        group = sd["param_groups"][0]
+        kind = "adam" if "betas" in group else ("sgd" if "dampening" in group else None)
+        if kind is not None and kind != self.kind:
+            raise ValueError(f"checkpoint holds {kind} optimizer state but --optimizer {self.kind} "
+                             f"was selected; pass --optimizer {kind}")
+
     # subclasses: step(grad_scale), state buffers, (de)serialisation
     def state_buffers(self) -> Dict[str, torch.Tensor]:
         raise NotImplementedError
@@ -134,6 +142,7 @@ class FlatAdam(FlatOptimizer):
         return {"state": state, "param_groups": self._torch_groups()}
 
     def load_state_dict(self, sd: dict) -> None:
+        self._check_kind(sd)
         group = sd["param_groups"][0]
         for k, v in group.items():
             if k != "params":
@@ -199,6 +208,7 @@ class FlatSGD(FlatOptimizer):
         return {"state": state, "param_groups": self._torch_groups()}
 
     def load_state_dict(self, sd: dict) -> None:
+        self._check_kind(sd)
         group = sd["param_groups"][0]
         for k, v in group.items():
             if k != "params":

@@ -11,7 +11,7 @@ def test_reference_defaults():
     assert a.init_method == "tcp://127.0.0.1:23456" and a.world_size == 1 and a.rank == 0
     assert a.seed is None
     # additions default to the reference behaviour
-    assert a.arch == "linear" and a.optimizer == "adam" and a.dtype == "fp32"
+    assert a.arch == "linear" and a.optimizer == "adam" and a.dtype == "auto"
 
 
 def test_short_and_alias_flags():

@@ -1,0 +1,68 @@
+"""The CLI end to end on one MI355X (BASELINE.json configs 2 and 4): CNN bf16 training with
+RCCL (ws=1), checkpoint, --resume + --evaluate on the GPU, and the same checkpoint evaluated
+on the CPU path (checkpoint format is device independent)."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import REPO, free_port
+
+pytestmark = pytest.mark.gpu
+EPOCH_RE = re.compile(r"^Epoch: (\d+)/(\d+), train loss: (\d+\.\d{6}), train acc: (\d+\.\d{2})%, "
+                      r"test loss: (\d+\.\d{6}), test acc: (\d+\.\d{2})%\.$")
+
+
+def cli(args, cwd, device="cuda", backend="nccl", timeout=600):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, os.path.join(REPO, "multi_proc_single_gpu.py"), "--device", device,
+           "--backend", backend, "-i", f"tcp://127.0.0.1:{free_port()}", "--synthetic"] + args
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout.splitlines()
+
+
+def test_cnn_cli_train_resume_evaluate(gpu, tmp_path):
+    out = cli(["--arch", "cnn", "--optimizer", "sgd", "--lr", "0.05", "--synthetic-size", "8192",
+               "--epochs", "2", "--seed", "1"], tmp_path)
+    ep = [EPOCH_RE.match(l) for l in out if l.startswith("Epoch:")]
+    assert len(ep) == 2 and all(ep), out
+    acc = [float(m.group(6)) for m in ep]
+    assert acc[1] > 80.0, out                           # synthetic data is learnable
+    ck = tmp_path / "checkpoints" / "checkpoint_1.pth.tar"
+    sd = torch.load(ck, weights_only=True)
+    assert sd["epoch"] == 2 and list(sd["state_dict"])[0] == "module.conv1.weight"
+    assert float(sd["optimizer"]["param_groups"][0]["lr"]) == pytest.approx(0.05)
+    # --evaluate --resume on the GPU reproduces the epoch's test line exactly
+    ev = [l for l in cli(["--arch", "cnn", "--optimizer", "sgd", "--evaluate", "--resume", str(ck)],
+                            tmp_path)
+          if l.startswith("test loss:")]
+    assert len(ev) == 1
+    assert ev[0] == "test loss: {}, test acc: {}%.".format(ep[1].group(5), ep[1].group(6))
+    # the same checkpoint on the CPU path (fp32) agrees to bf16 accuracy
+    evc = [l for l in cli(["--arch", "cnn", "--optimizer", "sgd", "--evaluate", "--resume", str(ck)],
+                          tmp_path, device="cpu", backend="gloo") if l.startswith("test loss:")]
+    m = re.match(r"test loss: (\d+\.\d+), test acc: (\d+\.\d+)%\.", evc[0])
+    assert abs(float(m.group(2)) - acc[1]) < 1.0
+    assert abs(float(m.group(1)) - float(ep[1].group(5))) < 0.02
+
+
+def test_linear_cli_gpu_matches_cpu(gpu, tmp_path):
+    """Reference default model (Linear, Adam, fp32) on the GPU path vs the CPU path."""
+    d1, d2 = tmp_path / "gpu", tmp_path / "cpu"
+    d1.mkdir()
+    d2.mkdir()
+    common = ["--synthetic-size", "4096", "--epochs", "2", "--seed", "2"]
+    g = [l for l in cli(common, d1) if l.startswith("Epoch:")]
+    c = [l for l in cli(common, d2, device="cpu", backend="gloo") if l.startswith("Epoch:")]
+    assert len(g) == len(c) == 2
+    for lg, lc in zip(g, c):
+        mg, mc = EPOCH_RE.match(lg), EPOCH_RE.match(lc)
+        for i in (3, 5):
+            assert abs(float(mg.group(i)) - float(mc.group(i))) < 2e-5, (lg, lc)
+        for i in (4, 6):
+            assert abs(float(mg.group(i)) - float(mc.group(i))) <= 0.05, (lg, lc)

@@ -1,4 +1,5 @@
 """Flat-arena optimizers == torch.optim on CPU (bitwise), and torch-format state dicts."""
+import pytest
 import torch
 
 from pytorch_distributed_mnist_amd.models import MODULES, get_spec
@@ -88,3 +89,16 @@ def test_sgd_state_dict_format():
     sd = ours.state_dict()
     assert sd["param_groups"][0].keys() == ref.state_dict()["param_groups"][0].keys()
     assert set(sd["state"][0]) == {"momentum_buffer"}
+
+
+def test_optimizer_kind_mismatch_is_reported():
+    from pytorch_distributed_mnist_amd.models.specs import get_spec
+    from pytorch_distributed_mnist_amd.optim.flat import FlatAdam, FlatSGD
+    from pytorch_distributed_mnist_amd.runtime.arena import FlatArena
+    arena = FlatArena(get_spec("linear"), torch.device("cpu"))
+    sgd_sd = FlatSGD(arena, lr=0.1, momentum=0.9).state_dict()
+    with pytest.raises(ValueError, match="--optimizer sgd"):
+        FlatAdam(arena, lr=1e-3).load_state_dict(sgd_sd)
+    adam_sd = FlatAdam(arena, lr=1e-3).state_dict()
+    with pytest.raises(ValueError, match="--optimizer adam"):
+        FlatSGD(arena, lr=0.1).load_state_dict(adam_sd)
