@@ -21,6 +21,8 @@
 //   conv_reduce: fixed-order slab sum -> conv gradients (bucket 1 complete).
 #include "cnn_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace cnn;
@@ -28,6 +30,10 @@ using namespace cnn;
 // ------------------------------------------------------------------ fc1_bwd
 constexpr int DW_TILES = FEAT / 64;  // 144
 constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
+constexpr int DX_COLS = 128;         // dX tile: 32 batch rows x 128 features per workgroup
+constexpr int DX_TILES = FEAT / DX_COLS;   // 72 = 8 XCDs x 9
+constexpr int NXCD = 8;              // MI355X: workgroups are dealt round-robin to 8 XCDs
+static_assert(DX_TILES % NXCD == 0 && DW_TILES % NXCD == 0, "XCD-aware tile mapping");
 constexpr int HR_BLOCKS = (HEAD_SLAB + 63) / 64;   // head-slab reduction workgroups (23)
 
 __device__ __forceinline__ int tile_off(int row, int byte) {  // [32 rows][128 B], 2-way-free tr reads
@@ -39,12 +45,12 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const bf16* __restrict__ pool, const bf16* __restrict__ wf1t, int B, float* __restrict__ gwf1,
     bf16* __restrict__ dpool, const float* __restrict__ head_slab, int head_blocks,
     float* __restrict__ gwf2, float* __restrict__ gbf2, float* __restrict__ gbf1,
-    double* __restrict__ metrics) {
+    double* __restrict__ metrics, int bid_offset) {
   __shared__ __attribute__((aligned(16))) char tile[DWC * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
-  const int nd = (ldt / 32) * DW_TILES;
-  const int bid = blockIdx.x;
+  const int nd = (ldt / 32) * DX_TILES;
+  const int bid = blockIdx.x + bid_offset;
 
   if (bid < DW_TILES) {
     // ---- dW1 tile: all 128 hidden rows x 64 feature columns, K = batch ----
@@ -90,6 +96,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         for (int kk = 0; kk < DWC / 32; ++kk) ac[mt][kk] = a[mt][kk];
       __syncthreads();
       if (c0 + DWC < ldt) load_chunk(c0 + DWC);
+      __builtin_amdgcn_sched_barrier(0);   // next chunk's loads stay ahead of this chunk's MFMAs
       const int nk = min(DWC / 32, (ldt - c0) / 32);
 #pragma unroll
       for (int kk = 0; kk < DWC / 32; ++kk) {
@@ -118,28 +125,57 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   }
 
   if (bid < DW_TILES + nd) {
-    // ---- dX tile: 32 batch rows x 64 feature columns, K = 128 hidden ----
+    // ---- dX tile: 32 batch rows x 128 features, K = 128 hidden ----
+    // Computed transposed, dpool^T[f][b] = W1^T[f][:] . dh^T[:][b]: the MFMA output lane then
+    // holds 4 consecutive features of one batch row, stored as one 8-byte bf16x4.  Each wave
+    // owns 32 features x 32 rows; all operand loads of the wave are issued up front.
+    // XCD-aware: workgroup t runs on XCD t % 8 (DW_TILES is a multiple of 8), and every XCD
+    // owns 1/8 of the feature range, so each XCD's L2 holds only its 1/8 of W1^T.
     const int t = bid - DW_TILES;
-    const int b0 = (t / DW_TILES) * 32, k0 = (t % DW_TILES) * 64 + wave * 16;
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    constexpr int TPX = DX_TILES / NXCD;                 // feature tiles per XCD
+    const int xcd = t % NXCD, loc = t / NXCD;
+    const int b0 = (loc / TPX) * 32;
+    const int f0 = (xcd * TPX + loc % TPX) * DX_COLS + wave * 32;
+    constexpr int FT = 2;
+    bf16x8 wa[FT][HID / 32], hb[2][HID / 32];
 #pragma unroll
     for (int ks = 0; ks < HID / 32; ++ks) {
-      const bf16x8 wv =
-          *reinterpret_cast<const bf16x8*>(wf1t + (int64_t)(k0 + i16) * HID + 32 * ks + 8 * g);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const bf16x8 av =
-            *reinterpret_cast<const bf16x8*>(dh + (int64_t)(b0 + mt * 16 + i16) * HID + 32 * ks + 8 * g);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wv, acc[mt], 0, 0, 0);
+      for (int ft = 0; ft < FT; ++ft)
+        wa[ft][ks] = *reinterpret_cast<const bf16x8*>(
+            wf1t + (int64_t)(f0 + ft * 16 + i16) * HID + 32 * ks + 8 * g);
+#pragma unroll
+      for (int bt = 0; bt < 2; ++bt)
+        hb[bt][ks] = *reinterpret_cast<const bf16x8*>(
+            dh + (int64_t)(b0 + bt * 16 + i16) * HID + 32 * ks + 8 * g);
+    }
+    // keep every load above this point: the scheduler would otherwise interleave them
+    // with the MFMAs behind per-load waits
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[FT][2];
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int bt = 0; bt < 2; ++bt) acc[ft][bt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HID / 32; ++ks)
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int bt = 0; bt < 2; ++bt)
+          acc[ft][bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ft][ks], hb[bt][ks], acc[ft][bt], 0, 0, 0);
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt) {
+      const int row = b0 + bt * 16 + i16;
+      if (row < B) {
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) {
+          const bf16x4 o = {to_bf16(acc[ft][bt][0]), to_bf16(acc[ft][bt][1]),
+                            to_bf16(acc[ft][bt][2]), to_bf16(acc[ft][bt][3])};
+          *reinterpret_cast<bf16x4*>(dpool + (int64_t)row * FEAT + f0 + ft * 16 + 4 * g) = o;
+        }
       }
     }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = b0 + mt * 16 + 4 * g + r;
-        if (row < B) dpool[(int64_t)row * FEAT + k0 + i16] = to_bf16(acc[mt][r]);
-      }
     return;
   }
 
@@ -156,6 +192,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         v[u] = head_slab[(int64_t)min(j0 + 4 * u, head_blocks - 1) * HEAD_SLAB + ec];
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const float x = (j0 + 4 * u < head_blocks) ? v[u] : 0.f;
@@ -230,6 +267,35 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
       mk[k] = mkv[it];
     }
   }
+  // conv1 operands, issued together with the image loads (unconditional clamped loads
+  // + selects: no per-load branch / wait)
+  float w1v[2][4];
+  int toff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int tap = 4 * g + j;
+    toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) w1v[mt][j] = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
+  }
+  f32x4 b1v[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  if (threadIdx.x == 0) PDM_STAMP_VAL(11, PDM_CLOCK());
+  // clear dz2 while the loads are in flight: the whole padded image for the first image
+  // (the border is never written), the interior for later ones (previous scatter)
+  if (first) {
+    for (int i = tid; i < DZW * DZW * 8; i += BWD_THREADS)
+      *reinterpret_cast<uint4*>(dzs + i * 16) = make_uint4(0, 0, 0, 0);
+  } else {
+    for (int i = tid; i < P2 * 8; i += BWD_THREADS) {
+      const int pix = i >> 3, r = pix / H2, c = pix - r * H2;
+      *reinterpret_cast<uint4*>(dzs + ((r + 2) * DZW + c + 2) * 128 + (i & 7) * 16) =
+          make_uint4(0, 0, 0, 0);
+    }
+  }
   if (tid < 196) {
     bf16x4 v = {to_bf16(pdm_normalize(xw & 0xff)), to_bf16(pdm_normalize((xw >> 8) & 0xff)),
                 to_bf16(pdm_normalize((xw >> 16) & 0xff)), to_bf16(pdm_normalize(xw >> 24))};
@@ -237,16 +303,7 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   } else if (tid < 200) {
     reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};
   }
-  if (threadIdx.x == 0) PDM_STAMP_VAL(11, PDM_CLOCK());
-  if (!first) {
-    // the previous image's scattered values must be cleared: zero the interior
-    for (int i = tid; i < P2 * 8; i += BWD_THREADS) {
-      const int pix = i >> 3, r = pix / H2, c = pix - r * H2;
-      *reinterpret_cast<uint4*>(dzs + ((r + 2) * DZW + c + 2) * 128 + (i & 7) * 16) =
-          make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-  }
+  __syncthreads();
   // scatter: each pooled gradient goes to its window's argmax pixel (if it was > 0);
   // dz2 is zero everywhere else.  For window pos s = 2dy + dx the padded pixel is
   // base + (dy*28 + dx) and its chunk swizzle (2r + c) & 7 is (b0 + s) & 7.
@@ -275,51 +332,173 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
     }
   }
   if (threadIdx.x == 0) PDM_STAMP_VAL(12, PDM_CLOCK());
-  // conv1 operands (loaded here rather than kept live across the role loops);
-  // unconditional clamped loads + selects: no per-load branch / wait
+  if (threadIdx.x == 448) PDM_STAMP_VAL(15, PDM_CLOCK());
   bf16x4 w1f[2];
-  int toff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tap = 4 * g + j;
-    toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const float wv = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
-      w1f[mt][j] = to_bf16(tap < 9 ? wv : 0.f);
-    }
-  }
-  f32x4 b1v[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
   __syncthreads();
-  // conv1 recompute: D[co][pixel] on mfma_f32_16x16x16_bf16 (same math as cnn_fwd)
-  for (int nt = wave; nt < (P1 + 15) / 16; nt += BWD_THREADS / 64) {
-    const int P = min(nt * 16 + i16, P1 - 1);
-    const int y = P / H1, x = P - y * H1;
-    const int xb = y * IMG + x;
-    bf16x4 bx;
+  if (threadIdx.x == 0) PDM_STAMP_VAL(13, PDM_CLOCK());
+  // conv1 recompute: D[co][pixel] on mfma_f32_16x16x16_bf16 (same math as cnn_fwd).
+  // 43 pixel tiles over 8 waves = 6 per wave (the last round clamps), every x read of
+  // the 6 tiles issued before their MFMAs.
+  constexpr int NT1 = (P1 + 15) / 16;                      // 43
+  constexpr int TPW = (NT1 + BWD_THREADS / 64 - 1) / (BWD_THREADS / 64);   // 6
+  bf16x4 bx[TPW];
+  int ty[TPW], tx[TPW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bx[j] = xs[toff[j] == IMG * IMG ? IMG * IMG : xb + toff[j]];
+  for (int k = 0; k < TPW; ++k) {
+    const int nt = min(wave + 8 * k, NT1 - 1);
+    const int P = min(nt * 16 + i16, P1 - 1);
+    ty[k] = P / H1;
+    tx[k] = P - ty[k] * H1;
+    const int xb = ty[k] * IMG + tx[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bx[k][j] = xs[toff[j] == IMG * IMG ? IMG * IMG : xb + toff[j]];
+  }
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int nt = wave + 8 * k;
+    const bool ok = nt < NT1 && nt * 16 + i16 < P1;
     uint32_t bits = 0;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx, b1v[mt], 0, 0, 0);
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
       bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
                   to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         bits |= (from_bf16(o[r]) > 0.f ? 1u : 0u) << (16 * mt + 4 * g + r);
-      if (nt * 16 + i16 < P1) *reinterpret_cast<bf16x4*>(a1s + a1_off(y, x, 32 * mt + 8 * g)) = o;
+      if (ok) *reinterpret_cast<bf16x4*>(a1s + a1_off(ty[k], tx[k], 32 * mt + 8 * g)) = o;
     }
     // relu' bitmask of the pixel: OR the 4 lane groups' channel bits
     bits |= __shfl_xor(bits, 16, 64);
     bits |= __shfl_xor(bits, 32, 64);
-    if (g == 0 && nt * 16 + i16 < P1) reinterpret_cast<uint32_t*>(smem + B_MK)[nt * 16 + i16] = bits;
+    if (g == 0 && ok) reinterpret_cast<uint32_t*>(smem + B_MK)[nt * 16 + i16] = bits;
   }
+  if (threadIdx.x == 0) PDM_STAMP_VAL(14, PDM_CLOCK());
 }
+
+// conv2 input gradient for MTP a1 pixel tiles {tile0 + 4k} of the staged image, fused with
+// relu'(a1) and the conv1 weight/bias gradient (accumulated into acc1).
+//   da1[p][ci] = sum_tap sum_co dz2[p - tap][co] * W2[co][tap][ci]
+// 18 straight-line (tap, K-half) steps; each W2^T fragment is loaded 4 steps ahead into its
+// own register and the dz2 A fragments one step ahead (double buffer).  Tiles past the
+// image (>= 43) compute on clamped pixels and are discarded by the epilogue.
+template <int MTP, int PF>
+__device__ __forceinline__ void dgrad_pass(const char* dzs, const uint32_t* mks, const bf16* xs,
+                                           const bf16* w2t, int tile0, f32x4 (&acc1)[2],
+                                           unsigned long long& t_mf, unsigned long long& t_ep) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
+  const unsigned long long c0 = PDM_CLOCK();
+  // opaque zero offset per pass: the W2^T loads must not be hoisted out of the pass loop.
+  // (Laundering the pointer itself would turn them into flat loads, which also count on
+  // lgkmcnt and make every LDS wait drain the in-flight global prefetch.)
+  int wz = 0;
+  asm volatile("" : "+s"(wz));
+  const bf16* w2l = w2t + wz;
+  auto wfrag = [&](int t, int kh, int nt) {
+    return *reinterpret_cast<const bf16x8*>(w2l + (t * C1 + nt * 16 + i16) * C2 + 32 * kh + 8 * g);
+  };
+  int dbase[MTP], s0[MTP];
+#pragma unroll
+  for (int k = 0; k < MTP; ++k) {
+    const int P = min((tile0 + 4 * k) * 16 + i16, P1 - 1);
+    const int y = P / H1, x = P - y * H1;
+    dbase[k] = ((y + 2) * DZW + x + 2) * 128;
+    s0[k] = 2 * y + x + 6;
+  }
+  f32x4 acc[MTP][2];
+#pragma unroll
+  for (int k = 0; k < MTP; ++k) acc[k][0] = acc[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 w[18][2];
+#pragma unroll
+  for (int tk = 0; tk < PF; ++tk) {
+    w[tk][0] = wfrag(tk >> 1, tk & 1, 0);
+    w[tk][1] = wfrag(tk >> 1, tk & 1, 1);
+  }
+  auto read_a = [&](int tk, bf16x8 (&a)[MTP]) {
+    const int t = tk >> 1, kh = tk & 1;
+    const int ky = t / 3, kx = t - 3 * ky;
+    const int toffb = (ky * DZW + kx) * 128;
+    const int gk = g + 4 * kh;
+    const int sk = 2 * ky + kx;
+#pragma unroll
+    for (int k = 0; k < MTP; ++k)
+      a[k] = *reinterpret_cast<const bf16x8*>(dzs + dbase[k] - toffb +
+                                              ((gk ^ ((s0[k] - sk) & 7)) << 4));
+  };
+  bf16x8 a[2][MTP];
+  read_a(0, a[0]);
+#pragma unroll
+  for (int tk = 0; tk < 18; ++tk) {
+    __builtin_amdgcn_sched_barrier(0);   // keep each step's loads where they are issued
+    if (tk + PF < 18) {
+      w[tk + PF][0] = wfrag((tk + PF) >> 1, (tk + PF) & 1, 0);
+      w[tk + PF][1] = wfrag((tk + PF) >> 1, (tk + PF) & 1, 1);
+    }
+    if (tk + 1 < 18) read_a(tk + 1, a[(tk + 1) & 1]);
+#pragma unroll
+    for (int k = 0; k < MTP; ++k) {
+      acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][0], acc[k][0], 0, 0, 0);
+      acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][1], acc[k][1], 0, 0, 0);
+    }
+  }
+  const unsigned long long c1 = PDM_CLOCK();
+  t_mf += c1 - c0;
+  // epilogue per tile: relu'(a1) bitmask -> dz1 (bf16) -> conv1 wgrad on
+  // mfma_f32_16x16x16_bf16 (M = ci, N = tap 0..8 / 9 = ones -> bias, K = pixels); the
+  // dgrad accumulator (lane: ci = 16nt + i16, pixels 4g + r) is already its A operand.
+  const int ctap = i16;
+  const int cky = ctap / 3, ckx = ctap - 3 * cky;
+  const int xoff = (ctap < 9) ? (cky * IMG + ckx) : IMG * IMG;
+  const bf16 one = to_bf16(1.f);
+#pragma unroll
+  for (int k = 0; k < MTP; ++k) {
+    const int P0 = (tile0 + 4 * k) * 16 + 4 * g;
+    const int y0 = P0 / H1, x0 = P0 - y0 * H1;
+    bf16x4 bx;
+    uint32_t mw[4];
+    bool valid[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool wrap = x0 + r >= H1;
+      const int yr = wrap ? y0 + 1 : y0, xr = wrap ? x0 + r - H1 : x0 + r;
+      valid[r] = P0 + r < P1;
+      const int yc = valid[r] ? yr : 0, xc = valid[r] ? xr : 0;
+      const int xi = (ctap < 9) ? yc * IMG + xc + xoff : IMG * IMG;
+      bx[r] = xs[xi];
+      mw[r] = mks[yc * H1 + xc];
+    }
+    if (ctap == 9) bx = bf16x4{one, one, one, one};
+    bf16x4 az[2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        az[nt][r] = to_bf16((valid[r] && ((mw[r] >> (16 * nt + i16)) & 1u)) ? acc[k][nt][r] : 0.f);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      acc1[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az[nt], bx, acc1[nt], 0, 0, 0);
+  }
+  t_ep += PDM_CLOCK() - c1;
+}
+
+// Work split (per image, after the staged load): waves 0-3 run the conv2 wgrad (18 (tap,
+// ci-tile) pairs), waves 4-7 the dgrad over 48 tile slots (43 real) in passes of DG_MTP.
+// PDM_DG_SPLIT=16 moves dgrad tiles 0..15 onto the wgrad waves when a workgroup has one
+// image.  Measured on MI355X (B=256, tools/kbench.py): split 0 / MTP 6 = 24.8 us, split 16 /
+// MTP 8 = 24.8 us, split 16 / MTP 4 = 27.3 us, split 0 / MTP 4 = 27.4 us: the balance does not
+// matter, the MFMAs per dgrad step do (the kernel is latency-bound at 2 waves per SIMD).
+#ifndef PDM_DG_SPLIT
+#define PDM_DG_SPLIT 0
+#endif
+constexpr int DG_SPLIT = PDM_DG_SPLIT;   // dgrad tiles done by the wgrad waves (0 or 16)
+#ifndef PDM_DG_MTP
+#define PDM_DG_MTP 6
+#endif
+constexpr int DG_MTP = PDM_DG_MTP;       // tiles per dgrad pass on waves 4-7
 
 __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     const uint8_t* __restrict__ xg, const float* __restrict__ w1, const float* __restrict__ b1,
@@ -336,13 +515,9 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
   const uint32_t* mks = reinterpret_cast<const uint32_t*>(smem + B_MK);
   float* out = slab + (int64_t)blockIdx.x * CONV_SLAB;
   float db2p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  unsigned long long t_mf = 0, t_ep = 0;
   PDM_STAMP(0);
-
-  // zero the whole padded dz2 image once: the border is never written, the interior
-  // only receives the scattered pooled gradients (re-zeroed for every further image)
-  for (int i = tid; i < DZW * DZW * 8; i += BWD_THREADS)
-    *reinterpret_cast<uint4*>(smem + B_DZ + i * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
 
   if (wave < 4) {
     // ===== conv2 weight gradient: (tap, ci-tile) pairs {w, w+4, ...} x all 4 co tiles =====
@@ -364,167 +539,88 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
       cpair[pi] = (ky * H1 + kx) * 64 + (((2 * nt + (pq >> 1)) ^ ((q + kx) & 3)) << 4) + 8 * (pq & 1);
     }
     const int u8b = 8 * (pq & 1);
-    for (int i = 0; i < ipb; ++i) {
-      const int img = blockIdx.x * ipb + i;
-      if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
+    auto wgrad_image = [&]() {
+#pragma unroll 2
+      for (int ks = 0; ks < P2 / 32; ++ks) {
+        const int c8 = ks * 4 + g;
+        const int row = c8 / 3;
+        const int x = (c8 - 3 * row) * 8 + q;
+        const int abase = (row * H1 + x) * 64;
+        const int dbase = ((row + 2) * DZW + x + 2) * 128 + u8b;
+        const int t = (((pq >> 1) ^ ((2 * row + x + 6) & 7)) << 4);
+        bf16x8 A[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          A[mt] = cat_tr(lds_tr16(dzs + dbase + ((32 * mt) ^ t)),
+                         lds_tr16(dzs + dbase + 512 + ((32 * mt) ^ t ^ 64)));
+#pragma unroll
+        for (int pi = 0; pi < 5; ++pi) {   // waves 2,3: pair 4 is a discarded duplicate
+          const bf16x8 Bv = cat_tr(lds_tr16(a1s + abase + cpair[pi]),
+                                   lds_tr16(a1s + abase + cpair[pi] + 256));
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mt], Bv, acc[pi][mt], 0, 0, 0);
+        }
+      }
+    };
+    // dW2[co][tap][ci]: rows co = 16mt + 4g + r, col ci = 16nt + i16
+    auto store_wgrad = [&]() {
+#pragma unroll
+      for (int pi = 0; pi < 5; ++pi) {
+        if (pi == 4 && !five) break;
+        const int pair = wave + 4 * pi;
+        const int tap = pair >> 1, nt = pair & 1;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + nt * 16 + i16] = acc[pi][mt][r];
+      }
+    };
+    if (ipb == 1) {
+      // one image: wgrad, store it (frees its 80 accumulators), then dgrad tiles 0..15
+      const int img = blockIdx.x;
+      if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, true, db2p);
       __syncthreads();
       PDM_STAMP(1);
       if (img < B) {
-#pragma unroll 2
-        for (int ks = 0; ks < P2 / 32; ++ks) {
-          const int c8 = ks * 4 + g;
-          const int row = c8 / 3;
-          const int x = (c8 - 3 * row) * 8 + q;
-          const int abase = (row * H1 + x) * 64;
-          const int dbase = ((row + 2) * DZW + x + 2) * 128 + u8b;
-          const int t = (((pq >> 1) ^ ((2 * row + x + 6) & 7)) << 4);
-          bf16x8 A[4];
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-            A[mt] = cat_tr(lds_tr16(dzs + dbase + ((32 * mt) ^ t)),
-                           lds_tr16(dzs + dbase + 512 + ((32 * mt) ^ t ^ 64)));
-#pragma unroll
-          for (int pi = 0; pi < 5; ++pi) {   // waves 2,3: pair 4 is a discarded duplicate
-            const bf16x8 Bv = cat_tr(lds_tr16(a1s + abase + cpair[pi]),
-                                     lds_tr16(a1s + abase + cpair[pi] + 256));
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-              acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mt], Bv, acc[pi][mt], 0, 0, 0);
-          }
-        }
+        wgrad_image();
+        PDM_STAMP(2);
+        store_wgrad();
+        if (DG_SPLIT > 0) dgrad_pass<(DG_SPLIT > 0 ? DG_SPLIT / 4 : 1), 4>(dzs, mks, xs, w2t, wave, acc1, t_mf, t_ep);
+      } else {
+        store_wgrad();
       }
-      PDM_STAMP(2);
-      __syncthreads();
       PDM_STAMP(3);
-    }
-    // dW2[co][tap][ci]: rows co = 16mt + 4g + r, col ci = 16nt + i16
-#pragma unroll
-    for (int pi = 0; pi < 5; ++pi) {
-      if (pi == 4 && !five) break;
-      const int pair = wave + 4 * pi;
-      const int tap = pair >> 1, nt = pair & 1;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + nt * 16 + i16] = acc[pi][mt][r];
+      __syncthreads();
+    } else {
+      // several images: the wgrad accumulators persist across them; dgrad is all on 4-7
+      for (int i = 0; i < ipb; ++i) {
+        const int img = blockIdx.x * ipb + i;
+        if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
+        __syncthreads();
+        PDM_STAMP(1);
+        if (img < B) wgrad_image();
+        PDM_STAMP(3);
+        __syncthreads();
+      }
+      store_wgrad();
     }
   } else {
     // ===== conv2 input gradient + relu'(a1) + conv1 weight/bias gradient =====
-    // Loop order (tap, K-half) outer, m-tile inner: the wave's 11 m-tiles keep their
-    // accumulators in registers for the whole image while only the 2 W2^T fragments of
-    // the current (tap, K-half) are live (prefetched one step ahead from L2), so the LDS
-    // reads of A can be issued well ahead of their MFMAs.
     const int wd = wave - 4;
-    constexpr int MTP = 6;                        // m-tiles per pass; 2 passes = 12 slots >= 11
-    // conv1 wgrad as a 16x16x16 MFMA: M = ci, N = tap (0..8; 9 = ones -> bias), K = pixels.
-    // The dgrad accumulator (lane: ci = i16, pixels 4g+r) is already its A operand.
-    const int ctap = i16;
-    const int cky = ctap / 3, ckx = ctap - 3 * cky;
-    const int xoff = (ctap < 9) ? (cky * IMG + ckx) : IMG * IMG;   // -> zero pad / ones
-    f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    const bf16 one = to_bf16(1.f);
-    const bf16* w2l = w2t;
-    auto wfrag = [&](int t, int kh, int nt) {
-      return *reinterpret_cast<const bf16x8*>(w2l + (t * C1 + nt * 16 + i16) * C2 + 32 * kh + 8 * g);
-    };
-    unsigned long long t_mf = 0, t_ep = 0;
     for (int i = 0; i < ipb; ++i) {
       const int img = blockIdx.x * ipb + i;
       if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
       __syncthreads();
       if (img < B) {
+        // tiles T0 + wd + 4j, j < (48 - T0) / 4, in passes of DG_MTP tiles; a rolled pass
+        // loop keeps one copy of the pass code and stops cross-pass scheduling
+        const int t0 = ipb > 1 ? 0 : DG_SPLIT;
+        const int n = (48 - t0) / 4;
 #pragma unroll 1
-        for (int pass = 0; pass < 2; ++pass) {
-          const unsigned long long c0 = PDM_CLOCK();
-          const int k0 = pass * MTP;
-          asm volatile("" : "+s"(w2l));   // opaque per pass: the W2^T loads must not be hoisted
-          // per-m-tile lane constants: padded-image pixel base and swizzle seed.  Slots past
-          // the wave's last real m-tile compute on clamped pixels and are discarded below.
-          int dbase[MTP], s0[MTP];
-#pragma unroll
-          for (int k = 0; k < MTP; ++k) {
-            const int P = min((wd + 4 * (k0 + k)) * 16 + i16, P1 - 1);
-            const int y = P / H1, x = P - y * H1;
-            dbase[k] = ((y + 2) * DZW + x + 2) * 128;
-            s0[k] = 2 * y + x + 6;
-          }
-          f32x4 acc[MTP][2];
-#pragma unroll
-          for (int k = 0; k < MTP; ++k) acc[k][0] = acc[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-          // straight-line (tap, K-half) steps; each W2^T fragment is loaded 4 steps ahead
-          // into its own register (no register rotation -> counted vmcnt waits)
-          bf16x8 w[18][2];
-#pragma unroll
-          for (int tk = 0; tk < 4; ++tk) {
-            w[tk][0] = wfrag(tk >> 1, tk & 1, 0);
-            w[tk][1] = wfrag(tk >> 1, tk & 1, 1);
-          }
-          // A fragments (dz2 rows) are read one step ahead into a second register set
-          auto read_a = [&](int tk, bf16x8 (&a)[MTP]) {
-            const int t = tk >> 1, kh = tk & 1;
-            const int ky = t / 3, kx = t - 3 * ky;
-            const int toffb = (ky * DZW + kx) * 128;
-            const int gk = g + 4 * kh;
-            const int sk = 2 * ky + kx;
-#pragma unroll
-            for (int k = 0; k < MTP; ++k)
-              a[k] = *reinterpret_cast<const bf16x8*>(
-                  dzs + dbase[k] - toffb + ((gk ^ ((s0[k] - sk) & 7)) << 4));
-          };
-          bf16x8 a[2][MTP];
-          read_a(0, a[0]);
-#pragma unroll
-          for (int tk = 0; tk < 18; ++tk) {
-            __builtin_amdgcn_sched_barrier(0);   // keep each step's loads where they are issued
-            if (tk + 4 < 18) {
-              w[tk + 4][0] = wfrag((tk + 4) >> 1, (tk + 4) & 1, 0);
-              w[tk + 4][1] = wfrag((tk + 4) >> 1, (tk + 4) & 1, 1);
-            }
-            if (tk + 1 < 18) read_a(tk + 1, a[(tk + 1) & 1]);
-#pragma unroll
-            for (int k = 0; k < MTP; ++k) {
-              acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][0], acc[k][0], 0, 0, 0);
-              acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][1], acc[k][1], 0, 0, 0);
-            }
-          }
-          const unsigned long long c1 = PDM_CLOCK();
-          t_mf += c1 - c0;
-          // epilogue per m-tile: relu'(a1) mask -> dz1 (bf16) -> conv1 wgrad MFMA.  Lane holds
-          // pixels 16mt + 4g + r for channel ci = 16nt + i16.  Branch-free: invalid pixels
-          // read pixel 0 and are zeroed by select.
-#pragma unroll
-          for (int k = 0; k < MTP; ++k) {
-            {
-              const int P0 = (wd + 4 * (k0 + k)) * 16 + 4 * g;
-              const int y0 = P0 / H1, x0 = P0 - y0 * H1;
-              bf16x4 bx;
-              uint32_t mw[4];
-              bool valid[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const bool wrap = x0 + r >= H1;
-                const int yr = wrap ? y0 + 1 : y0, xr = wrap ? x0 + r - H1 : x0 + r;
-                valid[r] = P0 + r < P1;
-                const int yc = valid[r] ? yr : 0, xc = valid[r] ? xr : 0;
-                const int xi = (ctap < 9) ? yc * IMG + xc + xoff : IMG * IMG;
-                bx[r] = xs[xi];
-                mw[r] = mks[yc * H1 + xc];
-              }
-              if (ctap == 9) bx = bf16x4{one, one, one, one};
-              bf16x4 az[2];
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
-                  az[nt][r] = to_bf16((valid[r] && ((mw[r] >> (16 * nt + i16)) & 1u)) ? acc[k][nt][r] : 0.f);
-#pragma unroll
-              for (int nt = 0; nt < 2; ++nt)
-                acc1[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az[nt], bx, acc1[nt], 0, 0, 0);
-            }
-          }
-          t_ep += PDM_CLOCK() - c1;
-        }
+        for (int ps = 0; ps * DG_MTP < n; ++ps)
+          dgrad_pass<DG_MTP, 4>(dzs, mks, xs, w2t, t0 + wd + 4 * DG_MTP * ps, acc1, t_mf, t_ep);
       }
       __syncthreads();
     }
@@ -533,12 +629,22 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
       PDM_STAMP_VAL(9, t_ep);
       PDM_STAMP_VAL(10, PDM_CLOCK());
     }
-    // acc1[nt]: rows ci = 16nt + 4g + r, col tap = i16
+  }
+  // conv1 weight/bias partials, acc1[nt]: rows ci = 16nt + 4g + r, col tap = i16.  Waves 4-7
+  // write their slot, waves 0-3 then add theirs (slot = wave & 3).
+  float* r1 = red + RED_DW1 + (wave & 3) * C1 * 16;
+  if (wave >= 4) {
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        red[RED_DW1 + wd * C1 * 16 + (nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
+      for (int r = 0; r < 4; ++r) r1[(nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) r1[(nt * 16 + 4 * g + r) * 16 + i16] += acc1[nt][r];
   }
   // conv2 bias: lanes sharing (lane & 7) hold the same 8 channels
 #pragma unroll
@@ -587,6 +693,7 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
     float4 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)min(j0 + 16 * u, nblk - 1) * STRIDE4];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const bool on = j0 + 16 * u < nblk;
@@ -617,9 +724,15 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
                     hipStream_t st) {
-  const int nblk = DW_TILES + (ldt / 32) * DW_TILES + HR_BLOCKS;
+  const int nd = (ldt / 32) * DX_TILES;
+  int nblk = DW_TILES + nd + HR_BLOCKS, off = 0;
+  // diagnostic only (tools/kbench.py): PDM_FC1BWD_ROLE=dw|dx|hr launches one role alone
+  static const char* role = getenv("PDM_FC1BWD_ROLE");
+  if (role && role[0] == 'd' && role[1] == 'w') nblk = DW_TILES;
+  else if (role && role[0] == 'd' && role[1] == 'x') { nblk = nd; off = DW_TILES; }
+  else if (role && role[0] == 'h') { nblk = HR_BLOCKS; off = DW_TILES + nd; }
   fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, dht, ldt, pool, wf1t, B, gwf1, dpool, head_slab,
-                                       head_blocks, gwf2, gbf2, gbf1, metrics);
+                                       head_blocks, gwf2, gbf2, gbf1, metrics, off);
 }
 
 int cnn_bwd_blocks(int B, int ipb) { return (B + ipb - 1) / ipb; }

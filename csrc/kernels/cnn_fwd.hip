@@ -185,7 +185,21 @@ constexpr int FC1_KB = 9;   // k-steps per load batch (288 k-steps = 32 batches)
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
                                                       float* __restrict__ part, int B, int kchunk) {
-  const int b0 = blockIdx.x * 32, sidx = blockIdx.y;
+  // XCD-aware mapping of the 1-D grid: workgroup w runs on XCD w % 8.  When the split
+  // count is a multiple of 8, every XCD owns S/8 splits (1/8 of W1's K range, for all
+  // m-tiles), so each XCD's L2 holds only its slice of W1 instead of all of it.
+  const int mtiles = (B + 31) / 32, S = FEAT / kchunk;
+  const int w = blockIdx.x;
+  int mtile, sidx;
+  if (S % 8 == 0) {
+    const int xcd = w % 8, loc = w / 8, spx = S / 8;
+    sidx = xcd * spx + loc % spx;
+    mtile = loc / spx;
+  } else {
+    sidx = w / mtiles;
+    mtile = w % mtiles;
+  }
+  const int b0 = mtile * 32;
   const int kbeg = sidx * kchunk;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rl = lane & 15, kg = (lane >> 4) * 8;
@@ -212,6 +226,7 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
       w0[i] = *reinterpret_cast<const bf16x8*>(pb0 + kb + 32 * i);
       w1[i] = *reinterpret_cast<const bf16x8*>(pb1 + kb + 32 * i);
     }
+    __builtin_amdgcn_sched_barrier(0);   // all loads of the batch before its MFMAs
 #pragma unroll
     for (int i = 0; i < FC1_KB; ++i) {
       acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w0[i], acc[0][0], 0, 0, 0);
@@ -270,6 +285,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
         for (int q = 0; q < 16; ++q)
           u[q] = reinterpret_cast<const float2*>(
               part + ((int64_t)min(s0 + q, S - 1) * B + rc) * HID)[j];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const bool on = s0 + q < S;
@@ -382,7 +398,7 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
 
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st) {
-  dim3 grid((B + 31) / 32, splitk);
+  dim3 grid(((B + 31) / 32) * splitk);
   fc1_fwd_kernel<<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);
 }
 

@@ -66,6 +66,9 @@ def compile_flags(abi: int, inc):
         flags.append("-DPDM_DEBUG_BOUNDS=1")
     if os.environ.get("PDM_STAMPS"):
         flags.append("-DPDM_STAMPS=1")
+    for k in ("PDM_DG_SPLIT", "PDM_DG_MTP"):          # tuning experiments (diagnostic builds)
+        if os.environ.get(k):
+            flags.append(f"-D{k}={int(os.environ[k])}")
     return flags
 
 

@@ -84,8 +84,11 @@ def init_distributed(backend: str, init_method: Optional[str], world_size: int, 
 
 
 def control_barrier() -> None:
+    """Host barrier on the control plane: an all-reduce of a CPU tensor always runs on the
+    gloo backend of the default group, so no torch NCCL communicator is ever created (a
+    plain ``dist.barrier()`` on a ``cpu:gloo,cuda:nccl`` group may pick the cuda backend)."""
     if distributed_is_initialized():
-        dist.barrier()
+        dist.all_reduce(torch.zeros(1))
 
 
 def shutdown() -> None:

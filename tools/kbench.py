@@ -12,15 +12,27 @@ test = synthetic_split(512, False)
 
 
 def timeit(fn, iters=50):
+    """GPU time per call: `iters` back-to-back calls captured into one hipGraph and replayed
+    (eager launches through the bindings would measure host overhead for small kernels)."""
     fn()
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
         fn()
-    e.record()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                fn()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(3):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / (3 * iters) * 1e3
 
 
 for B in [int(b) for b in (sys.argv[1:] or ["256", "1024", "4096"])]:
@@ -59,7 +71,7 @@ for B in [int(b) for b in (sys.argv[1:] or ["256", "1024", "4096"])]:
         us = timeit(fn)
         tot += us
         line.append(f"{name}={us:.1f}")
-    st.ctr.zero_()   # each step advances the data counter: stay inside the epoch buffer
-    step = timeit(lambda: st._train_impl(B), max(1, min(20, len(train) // B - 2)))
+    st.ctr.zero_()   # each step advances the data counter (rows are clamped past the epoch)
+    step = timeit(lambda: st._train_impl(B), 8)
     print(f"B={B:5d} S={S} ipb={ipb} " + " ".join(line) + f" | sum={tot:.1f}us step={step:.1f}us "
           f"-> {B / step * 1e6 / 1e6:.2f}M img/s", flush=True)

@@ -36,5 +36,8 @@ for which, names in (("fwd", ["start", "gathered(barrier)", "conv1(barrier)", "c
         print("   dgrad wave4: mfma-section cycles", st[:, 8].median().item(),
               " epilogue cycles", st[:, 9].median().item(),
               " dgrad done (rel)", (st[:, 10] - st[:, 0]).median().item())
-        print("   load: loads-landed (rel)", (st[:, 11] - st[:, 0]).median().item(),
-              " scatter done (rel)", (st[:, 12] - st[:, 0]).median().item())
+        print("   load: loads-issued (rel)", (st[:, 11] - st[:, 0]).median().item(),
+              " scatter done w0 / w7 (rel)", (st[:, 12] - st[:, 0]).median().item(),
+              (st[:, 15] - st[:, 0]).median().item(),
+              " post-scatter barrier", (st[:, 13] - st[:, 0]).median().item(),
+              " conv1 done w0", (st[:, 14] - st[:, 0]).median().item())
