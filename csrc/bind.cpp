@@ -125,7 +125,8 @@ void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tens
   need_aligned(out_images.data_ptr(), 16, "out_images");
   // indices are validated on the host by the caller (sampler output < N)
   launch_gather_epoch(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
-                      idx.data_ptr<int32_t>(), (int)n, out_images.data_ptr<uint8_t>(),
+                      idx.data_ptr<int32_t>(), (int)n, (int)images.size(0),
+                      out_images.data_ptr<uint8_t>(),
                       out_labels.data_ptr<int32_t>(), cur_stream(images));
 }
 

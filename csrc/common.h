@@ -46,6 +46,23 @@ __device__ __forceinline__ float from_bf16(bf16 h) { return (float)h; }
 // Bookkeeping done by exactly one thread of a kernel that no other kernel of the
 // same step reads concurrently (see runtime/gpu_step.py: the "middle" kernel
 // advances the data-step and optimizer-step counters).
+// Debug build only (PDM_DEBUG_BOUNDS=1 python -m pytorch_distributed_mnist_amd.build):
+// device-side index checks that print the failing site and trap; compiled out otherwise.
+#ifdef PDM_DEBUG_BOUNDS
+#define PDM_CHECK(cond, what, v0, v1)                                                      \
+  do {                                                                                     \
+    if (!(cond)) {                                                                         \
+      printf("PDM_CHECK failed: %s (%lld, %lld) block %d thread %d\n", what, (long long)(v0), \
+             (long long)(v1), (int)blockIdx.x, (int)threadIdx.x);                           \
+      __builtin_trap();                                                                    \
+    }                                                                                      \
+  } while (0)
+#else
+#define PDM_CHECK(cond, what, v0, v1) \
+  do {                                \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void pdm_bump_counters(int64_t* c0, int64_t* c1) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (c0) *c0 += 1;

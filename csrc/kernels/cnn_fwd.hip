@@ -51,7 +51,9 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   // anything else so its latency is not queued behind the weight loads.
   // sample row: sampler index (idx), epoch-buffer row (ctr only) or plain row (eval)
   // (clamped to the row space: a counter driven past the epoch reads a valid row)
-  const int64_t row = min(ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img, nrow - 1);
+  const int64_t row_u = ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img;
+  PDM_CHECK(row_u < nrow, "cnn_fwd sample row past the epoch", row_u, nrow);
+  const int64_t row = min(row_u, nrow - 1);
   const int64_t src = idx ? (int64_t)idx[row] : row;
   uint32_t xw = 0;
   if (tid < 196) xw = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];

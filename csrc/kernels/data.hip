@@ -10,11 +10,12 @@ namespace {
 __global__ __launch_bounds__(256) void gather_epoch_kernel(const uint8_t* __restrict__ images,
                                                            const int32_t* __restrict__ labels,
                                                            const int32_t* __restrict__ idx, int n,
-                                                           uint8_t* __restrict__ out_images,
+                                                           int nimg, uint8_t* __restrict__ out_images,
                                                            int32_t* __restrict__ out_labels) {
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
   if (row >= n) return;
   const int src = idx[row];
+  PDM_CHECK(src >= 0 && src < nimg, "gather_epoch index", src, nimg);
   const uint4* s = reinterpret_cast<const uint4*>(images + (int64_t)src * 784);
   uint4* d = reinterpret_cast<uint4*>(out_images + (int64_t)row * 784);
   for (int c = threadIdx.x & 15; c < 49; c += 16) d[c] = s[c];
@@ -24,7 +25,8 @@ __global__ __launch_bounds__(256) void gather_epoch_kernel(const uint8_t* __rest
 }  // namespace
 
 void launch_gather_epoch(const uint8_t* images, const int32_t* labels, const int32_t* idx, int n,
-                         uint8_t* out_images, int32_t* out_labels, hipStream_t st) {
+                         int nimg, uint8_t* out_images, int32_t* out_labels, hipStream_t st) {
   if (n <= 0) return;
-  gather_epoch_kernel<<<(n + 15) / 16, 256, 0, st>>>(images, labels, idx, n, out_images, out_labels);
+  gather_epoch_kernel<<<(n + 15) / 16, 256, 0, st>>>(images, labels, idx, n, nimg, out_images,
+                                                     out_labels);
 }

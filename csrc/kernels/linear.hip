@@ -91,6 +91,7 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
   const int row0 = blockIdx.x * ROWS;
   const int nrows = min(ROWS, B - row0);
   const int64_t base = (*ctr) * (int64_t)bfull;
+  PDM_CHECK(base + row0 + nrows <= nrow, "lin_train sample row past the epoch", base + row0, nrow);
   load_rows(xs, images, idx, base, row0, nrows, ROWS, true, nrow);
   __syncthreads();
 

@@ -84,6 +84,7 @@ def _hash(path, flags, hdr_digest):
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
           out: str | None = None) -> str:
     inc, lib, abi, _ = _torch_paths()
+    custom_out = out is not None
     flags = compile_flags(abi, inc)
     os.makedirs(OBJ_DIR, exist_ok=True)
     hd = hashlib.sha256()
@@ -133,7 +134,9 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     os.replace(out + ".tmp", out)
     # drop stale objects of sources that no longer exist / older hashes
     keep = set(objs)
-    for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not os.environ.get("PDM_STAMPS") else []:
+    variant = custom_out or any(os.environ.get(k) for k in
+                                     ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DG_SPLIT", "PDM_DG_MTP"))
+    for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not variant else []:
         if o not in keep:
             try:
                 os.unlink(o)

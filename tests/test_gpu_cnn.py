@@ -76,7 +76,7 @@ def test_cnn_forward_kernels(gpu, B):
     assert ((mask & 3) == ref_s)[clear & pos].all()
 
 
-@pytest.mark.parametrize("B", [64, 40])
+@pytest.mark.parametrize("B", [64, 40, 300])
 def test_cnn_step_gradients_match_autograd(gpu, B):
     prog, train, _ = _program(B)      # SGD lr=0: params unchanged, grads left in the arena
     idx = distributed_indices(len(train), 1, 0, 0)
@@ -147,3 +147,23 @@ def test_cnn_trains_and_tracks_cpu(gpu, graphs):
         el, ea = p.evaluate()
         hist.append((tl.average, el.average, ea.accuracy))
     assert hist[-1][0] < hist[0][0] and hist[-1][2] > 0.8, hist
+
+
+def test_cnn_large_batch_steps(gpu):
+    """BASELINE config 5 shape: batch 8192 per rank (several images per conv-backward
+    workgroup, split-K 1), graph-captured, over an enlarged synthetic set, incl. the ragged
+    tail step of the epoch."""
+    n = 8192 * 2 + 1000
+    train = synthetic_split(n, True)
+    test = synthetic_split(512, False)
+    p = build_local_program("cnn", "bf16", "cuda", 8192, train, test, optimizer="sgd", lr=0.05,
+                            momentum=0.9, seed=1, use_graphs=True)
+    p.optimizer.sync_hyperparams()
+    p.set_train_indices(distributed_indices(n, 1, 0, 0))
+    tl, ta = p.train_epoch()                 # 2 full steps + a 1000-image tail
+    assert tl.count == n
+    assert torch.isfinite(p.arena.params).all()
+    assert int(p.gpu.ctr[0].item()) == 3
+    p.set_train_indices(distributed_indices(n, 1, 0, 1))
+    tl2, _ = p.train_epoch()
+    assert tl2.count == n and tl2.average < tl.average, (tl.average, tl2.average)
