@@ -30,6 +30,7 @@ from .models.specs import get_spec
 from .optim.flat import adjust_learning_rate, build_optimizer
 from .runtime.arena import FlatArena
 from .runtime.program import TrainProgram
+from .utils import trace
 from .utils.checkpoint import load_checkpoint, make_state, save_checkpoint
 
 best_acc = 0
@@ -91,6 +92,8 @@ def run(args):
     ctx = build_rank_state(args, rank, world_size, local_rank)
     device = ctx.device
     out = _printer(rank, args.rank_prefix)
+    if getattr(args, "trace", False):
+        trace.enable(True)
 
     # Reference splits the node batch by the GPU count (:170-175); the GPU count
     # equals world_size under its assert, and world_size is what we divide by.
@@ -142,27 +145,30 @@ def run(args):
             return
 
         for epoch in range(args.start_epoch, args.epochs):
-            program.set_train_indices(
-                sampler.distributed_indices(len(train_split), world_size, rank, epoch))
-            adjust_learning_rate(optimizer, epoch, args)
+            with trace.range("epoch {}".format(epoch)):
+                with trace.range("sampler upload"):
+                    program.set_train_indices(
+                        sampler.distributed_indices(len(train_split), world_size, rank, epoch))
+                adjust_learning_rate(optimizer, epoch, args)
 
-            train_loss, train_acc = trainer.train()
-            test_loss, test_acc = trainer.evaluate()
+                train_loss, train_acc = trainer.train()
+                test_loss, test_acc = trainer.evaluate()
 
-            out('Epoch: {}/{},'.format(epoch, args.epochs),
-                'train loss: {}, train acc: {},'.format(train_loss, train_acc),
-                'test loss: {}, test acc: {}.'.format(test_loss, test_acc))
-            if args.perf and rank == 0:
-                n = train_loss.count * world_size
-                out("perf: epoch {} train {:.1f} img/s (node, {} samples in {:.4f}s), "
-                    "eval {:.4f}s".format(epoch, n / max(trainer.last_train_seconds, 1e-12), n,
-                                          trainer.last_train_seconds, trainer.last_eval_seconds))
+                out('Epoch: {}/{},'.format(epoch, args.epochs),
+                    'train loss: {}, train acc: {},'.format(train_loss, train_acc),
+                    'test loss: {}, test acc: {}.'.format(test_loss, test_acc))
+                if args.perf and rank == 0:
+                    n = train_loss.count * world_size
+                    out("perf: epoch {} train {:.1f} img/s (node, {} samples in {:.4f}s), "
+                        "eval {:.4f}s".format(epoch, n / max(trainer.last_train_seconds, 1e-12), n,
+                                              trainer.last_train_seconds, trainer.last_eval_seconds))
 
-            is_best = test_acc.accuracy > best_acc
-            best_acc = max(test_acc.accuracy, best_acc)
-            if rank == 0:
-                save_checkpoint(make_state(epoch + 1, arena, best_acc, optimizer), is_best, epoch,
-                                directory=args.checkpoint_dir)
+                is_best = test_acc.accuracy > best_acc
+                best_acc = max(test_acc.accuracy, best_acc)
+                if rank == 0:
+                    with trace.range("checkpoint"):
+                        save_checkpoint(make_state(epoch + 1, arena, best_acc, optimizer), is_best,
+                                        epoch, directory=args.checkpoint_dir)
     finally:
         comm.close()
         parallel.shutdown()

@@ -77,6 +77,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help='process-group / rendezvous timeout in seconds')
     g.add_argument('--perf', action='store_true',
                    help='print an extra per-epoch throughput line on rank 0')
+    g.add_argument('--trace', action='store_true',
+                   help='emit roctx ranges (epoch/train/evaluate/checkpoint) for rocprofv3 '
+                        '--marker-trace')
     g.add_argument('--rank-prefix', action='store_true',
                    help="prefix every per-rank line with '[rank r] '")
     parser.set_defaults(local_rank_given=False)

@@ -12,6 +12,8 @@ import time
 
 import torch
 
+from .utils import trace
+
 
 class Trainer:
     def __init__(self, program):
@@ -26,12 +28,14 @@ class Trainer:
     def train(self):
         self._sync()
         t0 = time.perf_counter()
-        result = self.program.train_epoch()   # reading the metrics synchronises
+        with trace.range("train"):
+            result = self.program.train_epoch()   # reading the metrics synchronises
         self.last_train_seconds = time.perf_counter() - t0
         return result
 
     def evaluate(self):
         t0 = time.perf_counter()
-        result = self.program.evaluate()
+        with trace.range("evaluate"):
+            result = self.program.evaluate()
         self.last_eval_seconds = time.perf_counter() - t0
         return result
