@@ -58,17 +58,8 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   uint32_t xw = 0;
   if (tid < 196) xw = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];
   if (tid == 0) ylab[img] = labels[src];
+  if (tid == 0) PDM_STAMP_VAL(8, PDM_CLOCK());   // image load issued
 
-  // conv2 B fragments for this wave's two n-tiles (co = 32*(wave&1) + 16*j + i16):
-  // lane l holds B[k = ci = 8g + e][n = co] = w2[co][tap][ci]
-  const int nh = wave & 1;
-  bf16x8 wb[9][2];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      wb[t][j] = *reinterpret_cast<const bf16x8*>(
-          w2 + ((nh * 32 + j * 16 + i16) * 9 + t) * 32 + 8 * g);
   // conv1 as D[co][pixel] = W1[co][tap] . X[tap][pixel] on mfma_f32_16x16x16_bf16:
   // A = weights (lane row co = i16, k = taps 4g..4g+3, zero past tap 8), B = input
   // patches (lane col = pixel, k = taps); bias is the initial accumulator.
@@ -89,15 +80,28 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  // conv2 B fragments for this wave's two n-tiles (co = 32*(wave&1) + 16*j + i16):
+  // lane l holds B[k = ci = 8g + e][n = co] = w2[co][tap][ci].  Issued after every load
+  // conv1 needs: global loads retire in order (vmcnt), so conv1 does not wait for these
+  // 18 KB per wave, which stream in while the image is normalised and conv1 runs.
+  const int nh = wave & 1;
   float b2r[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) b2r[j] = b2[nh * 32 + j * 16 + i16];
+  bf16x8 wb[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      wb[t][j] = *reinterpret_cast<const bf16x8*>(
+          w2 + ((nh * 32 + j * 16 + i16) * 9 + t) * 32 + 8 * g);
 
   if (tid < 196) {
     bf16x4 v = {to_bf16(pdm_normalize(xw & 0xff)), to_bf16(pdm_normalize((xw >> 8) & 0xff)),
                 to_bf16(pdm_normalize((xw >> 16) & 0xff)), to_bf16(pdm_normalize(xw >> 24))};
     reinterpret_cast<bf16x4*>(xs)[tid] = v;
     if (TRAIN) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[tid] = xw;
+    if (tid == 0) PDM_STAMP_VAL(9, PDM_CLOCK());   // image landed
   } else if (tid < 200) {
     reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};   // zero pad (taps 9..15)
   }
