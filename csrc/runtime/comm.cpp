@@ -170,10 +170,13 @@ class GradReducer {
     }
     ready_.resize(starts_.size());
     for (auto& e : ready_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    reduced_.resize(starts_.size());
+    for (auto& e : reduced_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   }
   ~GradReducer() {
     for (auto& e : ready_) hipEventDestroy(e);
+    for (auto& e : reduced_) hipEventDestroy(e);
     hipEventDestroy(done_);
   }
 
@@ -184,7 +187,15 @@ class GradReducer {
     HIP_OK(hipStreamWaitEvent(comm_.stream(), ready_[i], 0));
     float* base = grads_.data_ptr<float>() + starts_[i];
     comm_.all_reduce_range(base, (size_t)counts_[i], ncclFloat32);
+    HIP_OK(hipEventRecord(reduced_[i], comm_.stream()));
     pending_ = true;
+  }
+
+  // make the caller's current stream wait for bucket i's all-reduce only (e.g. a side
+  // stream running that bucket's optimizer while later backward kernels still run)
+  void wait_bucket(int i) {
+    TORCH_CHECK(i >= 0 && i < (int)starts_.size(), "bad bucket index");
+    HIP_OK(hipStreamWaitEvent(comm_.caller(), reduced_[i], 0));
   }
 
   void finalize() {
@@ -201,7 +212,7 @@ class GradReducer {
   RcclComm& comm_;
   at::Tensor grads_;
   std::vector<int64_t> starts_, counts_;
-  std::vector<hipEvent_t> ready_;
+  std::vector<hipEvent_t> ready_, reduced_;
   hipEvent_t done_ = nullptr;
   bool pending_ = false;
 };
@@ -228,5 +239,6 @@ void register_comm(py::module& m) {
       .def(py::init<RcclComm&, at::Tensor, std::vector<int64_t>>(), py::keep_alive<1, 2>())
       .def("bucket_ready", &GradReducer::bucket_ready)
       .def("finalize", &GradReducer::finalize)
+      .def("wait_bucket", &GradReducer::wait_bucket)
       .def_property_readonly("num_buckets", &GradReducer::num_buckets);
 }

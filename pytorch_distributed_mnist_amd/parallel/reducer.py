@@ -37,7 +37,7 @@ class GradReducer:
         self.active = force or comm.world_size > 1
         self.grad_scale = 1.0 / comm.world_size
         self._native = None
-        self._pending = []
+        self._pending = {}
         if self.active and isinstance(comm, RcclComm):
             C = _ext.require()
             flat = [b for se in self.bounds for b in se]
@@ -56,9 +56,20 @@ class GradReducer:
         s, e = self.bounds[i]
         view = self.grads[s:e]
         if isinstance(self.comm, TorchComm):
-            self._pending.append(self.comm.all_reduce_(view, async_op=True))
+            self._pending[i] = self.comm.all_reduce_(view, async_op=True)
         else:
             self.comm.all_reduce_(view)
+
+    def wait_bucket(self, i: int) -> None:
+        """Make the current stream (or the host, on the torch path) wait for bucket i only."""
+        if not self.active:
+            return
+        if self._native is not None:
+            self._native.wait_bucket(i)
+            return
+        w = self._pending.pop(i, None)
+        if w is not None:
+            w.wait()
 
     def finalize(self) -> None:
         if not self.active:
@@ -66,7 +77,7 @@ class GradReducer:
         if self._native is not None:
             self._native.finalize()
             return
-        for w in self._pending:
+        for w in self._pending.values():
             w.wait()
         self._pending.clear()
 

@@ -136,9 +136,11 @@ class GpuStepBase:
         """[(offset, rows, cols, shadow|None, shadow_t|None)] covering the arena."""
         return [(0, 1, self.arena.spec.total, None, None)]
 
-    def launch_optimizer(self) -> None:
+    def launch_optimizer(self, segments=None) -> None:
+        """One fused optimizer launch over `segments` (default: every parameter)."""
         if self._opt_segments is None:
             self._opt_segments = self.optimizer_segments()
+        segs = self._opt_segments if segments is None else segments
         o = self.opt
         g = o.param_groups[0]
         if o.kind == "adam":
@@ -146,13 +148,13 @@ class GpuStepBase:
             self.C.optim_step(self.C.OPT_ADAM, self.arena.params, self.arena.grads, o.exp_avg,
                               o.exp_avg_sq, o._lr_dev, o._step_dev, float(b1), float(b2),
                               float(g["eps"]), float(g["weight_decay"]), 0.0, 0.0, False,
-                              float(self.reducer.grad_scale), self._opt_segments)
+                              float(self.reducer.grad_scale), segs)
         else:
             self.C.optim_step(self.C.OPT_SGD, self.arena.params, self.arena.grads,
                               o.momentum_buffer, None, o._lr_dev, o._step_dev, 0.0, 0.0, 0.0,
                               float(g["weight_decay"]), float(g["momentum"]),
                               float(g["dampening"]), bool(g["nesterov"]),
-                              float(self.reducer.grad_scale), self._opt_segments)
+                              float(self.reducer.grad_scale), segs)
 
     def invalidate_graphs(self) -> None:
         self.graphs.clear()
