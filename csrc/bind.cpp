@@ -131,7 +131,8 @@ void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tens
 }
 
 // ------------------------------------------------------------------ optimizer
-// segs: list of (offset, rows, cols, shadow or None, shadow_t or None)
+// segs: list of (offset, rows, cols, shadow or None, shadow_t or None
+//                [, (slab, nslab, col0, stride) or None])
 void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::optional<at::Tensor> v,
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd,
                 double momentum, double dampening, bool nesterov, double grad_scale,
@@ -180,6 +181,25 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
     TORCH_CHECK(s.offset % 4 == 0, "segment offsets must be 16-byte aligned");
     s.shadow = nullptr;
     s.shadow_t = nullptr;
+    s.slab = nullptr;
+    s.nslab = 0;
+    s.slab_col0 = 0;
+    s.slab_stride = 0;
+    if (t.size() > 5 && !t[5].is_none()) {
+      // (slab tensor, nslab, col0, stride): gradient = fixed-order sum over the slabs
+      auto sl = t[5].cast<py::tuple>();
+      auto st = sl[0].cast<at::Tensor>();
+      need(st, at::kFloat, "gradient slab");
+      s.nslab = (int32_t)sl[1].cast<int64_t>();
+      s.slab_col0 = (int32_t)sl[2].cast<int64_t>();
+      s.slab_stride = sl[3].cast<int64_t>();
+      const int64_t numel = (int64_t)s.rows * s.cols;
+      TORCH_CHECK(s.nslab >= 1 && numel % 4 == 0 && s.slab_col0 % 4 == 0 && s.slab_stride % 4 == 0 &&
+                      s.slab_col0 + numel <= s.slab_stride &&
+                      st.numel() >= (int64_t)s.nslab * s.slab_stride, "gradient slab geometry");
+      need_aligned(st.data_ptr(), 16, "gradient slab");
+      s.slab = st.data_ptr<float>();
+    }
     if (!t[3].is_none()) {
       auto sh = t[3].cast<at::Tensor>();
       need(sh, at::kBFloat16, "shadow");
@@ -382,6 +402,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });
   m.attr("CNN_HEAD_SLAB") = CNN_HEAD_SLAB;
   m.attr("CNN_CONV_SLAB") = CNN_CONV_SLAB;
+  m.attr("CNN_CONV_SLAB_DB2") = CNN_CONV_SLAB_DB2;
+  m.attr("CNN_CONV_SLAB_DW1") = CNN_CONV_SLAB_DW1;
+  m.attr("CNN_CONV_SLAB_DB1") = CNN_CONV_SLAB_DB1;
   m.def("cnn_fwd", &cnn_fwd);
   m.def("fc1_fwd", &fc1_fwd);
   m.def("cnn_head", &cnn_head);

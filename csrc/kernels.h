@@ -34,6 +34,12 @@ struct OptSeg {
   int32_t first_block; // filled by launch_optim
   __bf16* shadow;      // optional bf16 copy, same layout
   __bf16* shadow_t;    // optional bf16 copy, transposed [cols][rows]
+  // optional: the gradient is the fixed-order sum of `nslab` per-workgroup slabs
+  // (row stride `slab_stride` floats, this segment at column `slab_col0`) — the
+  // conv_reduce pass fused into the update (world_size 1: no all-reduce in between)
+  const float* slab;
+  int32_t nslab, slab_col0;
+  int64_t slab_stride;
 };
 
 struct OptArgs {
@@ -71,6 +77,9 @@ constexpr int CNN_HEAD_MAX_BLOCKS = 256;  // head workgroups (grid-stride over r
 int cnn_head_blocks(int groups);          // head workgroups = head slabs for `groups` row groups
 constexpr int CNN_HEAD_SLAB = 1420;   // 1280 dWfc2 + 10 dbfc2 + 128 dbfc1 + loss + correct
 constexpr int CNN_CONV_SLAB = 18816;  // 18432 dW2 + 64 db2 + 288 dW1 + 32 db1
+constexpr int CNN_CONV_SLAB_DB2 = 18432;   // slab column of db2 ([co][tap][ci] dW2 before it)
+constexpr int CNN_CONV_SLAB_DW1 = 18496;   // dW1 [32][9]
+constexpr int CNN_CONV_SLAB_DB1 = 18784;   // db1 [32]
 
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                     int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,

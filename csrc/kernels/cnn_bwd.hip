@@ -230,6 +230,8 @@ constexpr int B_TOTAL = B_MK + P1 * 4;           // 158160 B -> 1 workgroup / CU
 constexpr int SL_DB2 = C2 * 9 * C1;             // 18432
 constexpr int SL_DW1 = SL_DB2 + C2;             // 18496
 constexpr int SL_DB1 = SL_DW1 + C1 * 9;         // 18784
+static_assert(SL_DB2 == CNN_CONV_SLAB_DB2 && SL_DW1 == CNN_CONV_SLAB_DW1 &&
+              SL_DB1 == CNN_CONV_SLAB_DB1 && SL_DB1 + C1 == CNN_CONV_SLAB, "conv slab layout");
 
 // dz2 padded image: pixel (r, c) in [0,28)^2 holds dz2[r-2][c-2] (0 on the border), 128 B,
 // 16-B chunk XOR (2r + c) & 7: dgrad row reads conflict-free, wgrad transposed reads 2-way.

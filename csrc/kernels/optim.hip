@@ -52,6 +52,9 @@ __device__ __forceinline__ Hyper make_hyper(const OptArgs& a) {
 template <int KIND>
 __device__ __forceinline__ float update(float p, float g, float& m, float& v, const Hyper& h,
                                         float gs) {
+  // torch rounds after every op (mul_, add_, addcmul_, ...): no FMA contraction, which
+  // also keeps every code path of this kernel bit-identical
+#pragma clang fp contract(off)
   g *= gs;
   if (h.wd != 0.f) g = fmaf(h.wd, p, g);  // grad.add(param, alpha=wd)
   if (KIND == OPT_ADAM) {
@@ -85,6 +88,53 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   float* __restrict__ M = a.m + s.offset;
   float* __restrict__ V = (KIND == OPT_ADAM) ? a.v + s.offset : nullptr;
   const int64_t numel = (int64_t)s.rows * s.cols;
+
+  if (s.slab != nullptr) {
+    // slab-reduced segment: 64 elements per workgroup; lane c4 = tid & 15 owns 4 of them
+    // (float4), group rg = tid >> 4 sums slabs rg, rg + 16, ... (8 loads in flight), and
+    // the 16 group sums are combined in a fixed order (the conv_reduce order, bit for bit)
+    __shared__ float4 red[16][16];
+    const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
+    const int e0 = lb * 64;
+    const int col = s.slab_col0 + min(e0 + 4 * c4, (int)numel - 4);   // clamped: stays in row
+    const float4* sp = reinterpret_cast<const float4*>(s.slab + col);
+    const int64_t st4 = s.slab_stride / 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j0 = rg; j0 < s.nslab; j0 += 16 * 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)min(j0 + 16 * u, s.nslab - 1) * st4];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool on = j0 + 16 * u < s.nslab;
+        acc.x += on ? v[u].x : 0.f;
+        acc.y += on ? v[u].y : 0.f;
+        acc.z += on ? v[u].z : 0.f;
+        acc.w += on ? v[u].w : 0.f;
+      }
+    }
+    red[rg][c4] = acc;
+    __syncthreads();
+    const int e = e0 + tid;
+    if (tid < 64 && e < numel) {
+      // numel % 4 == 0, so a valid element's float4 group is never a clamped one
+      const float* rf = reinterpret_cast<const float*>(&red[0][0]);
+      float gsum = 0.f;
+#pragma unroll
+      for (int gq = 0; gq < 16; ++gq) gsum += rf[gq * 64 + tid];
+      const_cast<float*>(G)[e] = gsum;              // the reduced gradient stays observable
+      float m = M[e], v = (KIND == OPT_ADAM) ? V[e] : 0.f;
+      const float p = update<KIND>(P[e], gsum, m, v, h, a.grad_scale);
+      P[e] = p;
+      M[e] = m;
+      if (KIND == OPT_ADAM) V[e] = v;
+      const bf16 hb = to_bf16(p);
+      if (s.shadow) s.shadow[e] = hb;
+      if (s.shadow_t) s.shadow_t[(int64_t)(e % s.cols) * s.rows + e / s.cols] = hb;
+    }
+    return;
+  }
 
   if (s.shadow_t == nullptr) {
     // plain segment: 8 contiguous floats per thread (2 x float4)
@@ -199,6 +249,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
 }  // namespace
 
 int opt_blocks_for(const OptSeg& s) {
+  if (s.slab) return (int)(((int64_t)s.rows * s.cols + 63) / 64);
   if (s.shadow_t) return ((s.rows + TR - 1) / TR) * ((s.cols + TC - 1) / TC);
   const int64_t n = (int64_t)s.rows * s.cols;
   return (int)((n + CHUNK - 1) / CHUNK);

@@ -85,6 +85,11 @@ class CnnStep(GpuStepBase):
         # concurrent with the conv backward.  Measured on MI355X at B=256 it is slower
         # (90.6 vs 74.7 us/step: its workgroups take CUs ahead of cnn_bwd), so it is off.
         self.split_opt = os.environ.get("PDM_SPLIT_OPT", "0") == "1"
+        # world_size 1 (no all-reduce between backward and update): the conv gradient
+        # reduction is fused into the optimizer launch (PDM_FUSE_CONV_REDUCE=0 disables)
+        self.fuse_conv_reduce = (not self.reducer.active and not self.split_opt and
+                                 os.environ.get("PDM_FUSE_CONV_REDUCE", "1") != "0")
+        self._fused = {}
         self.side = torch.cuda.Stream(device=dev)
         self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
         self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
@@ -138,6 +143,27 @@ class CnnStep(GpuStepBase):
     def invalidate_graphs(self) -> None:
         super().invalidate_graphs()
         self._bsegs = None
+        self._fused = {}
+
+    def _fused_segments(self, nblk: int):
+        """Optimizer segments whose conv gradients are summed from `nblk` cnn_bwd slabs."""
+        segs = self._fused.get(nblk)
+        if segs is None:
+            if self._opt_segments is None:
+                self._opt_segments = self.optimizer_segments()
+            C = self.C
+            col = {"conv2.weight": 0, "conv2.bias": C.CNN_CONV_SLAB_DB2,
+                   "conv1.weight": C.CNN_CONV_SLAB_DW1, "conv1.bias": C.CNN_CONV_SLAB_DB1}
+            by_off = {self.arena.spec.offset(n): n for n in col}
+            segs = []
+            for sg in self._opt_segments:
+                name = by_off.get(sg[0])
+                if name is None:
+                    segs.append(sg)
+                else:
+                    segs.append(tuple(sg) + ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),))
+            self._fused[nblk] = segs
+        return segs
 
     def _train_impl(self, B: int) -> None:
         C, P, G = self.C, self.P, self.G
@@ -165,6 +191,9 @@ class CnnStep(GpuStepBase):
         ipb = choose_ipb(B)
         C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
                   ipb, self.conv_slab)
+        if self.fuse_conv_reduce:
+            self.launch_optimizer(self._fused_segments(C.cnn_bwd_nblk(B, ipb)))
+            return
         C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
         self.reducer.bucket_ready(1)

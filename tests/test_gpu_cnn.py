@@ -167,3 +167,20 @@ def test_cnn_large_batch_steps(gpu):
     p.set_train_indices(distributed_indices(n, 1, 0, 1))
     tl2, _ = p.train_epoch()
     assert tl2.count == n and tl2.average < tl.average, (tl.average, tl2.average)
+
+
+def test_fused_conv_reduce_matches_separate_pass(gpu):
+    """world_size 1 folds the conv slab reduction into the optimizer launch; it must give the
+    same bits as conv_reduce + optimizer (same fixed summation order), incl. a tail step."""
+    res = []
+    for fuse in (True, False):
+        prog, train, _ = _program(96, lr=0.05, n=96 * 3 + 40, seed=5)
+        prog.gpu.fuse_conv_reduce = fuse
+        prog.gpu.invalidate_graphs()
+        prog.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        prog.train_epoch()
+        torch.cuda.synchronize()
+        res.append((prog.arena.params.clone(), prog.arena.grads.clone(),
+                    prog.optimizer.momentum_buffer.clone()))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
