@@ -155,13 +155,17 @@ class CnnStep(GpuStepBase):
             col = {"conv2.weight": 0, "conv2.bias": C.CNN_CONV_SLAB_DB2,
                    "conv1.weight": C.CNN_CONV_SLAB_DW1, "conv1.bias": C.CNN_CONV_SLAB_DB1}
             by_off = {self.arena.spec.offset(n): n for n in col}
-            segs = []
+            slab_segs, plain = [], []
             for sg in self._opt_segments:
                 name = by_off.get(sg[0])
                 if name is None:
-                    segs.append(sg)
+                    plain.append(sg)
                 else:
-                    segs.append(tuple(sg) + ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),))
+                    slab_segs.append(tuple(sg) +
+                                     ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),))
+            # slab segments first: their workgroups (a 256-deep reduction each) are
+            # dispatched before the streaming fc updates instead of forming the tail
+            segs = slab_segs + plain
             self._fused[nblk] = segs
         return segs
 
