@@ -1,0 +1,29 @@
+"""bench.py driver contract on one MI355X: one JSON line with the BASELINE metric/config."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_json_contract(gpu):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20",
+                        "--warmup", "3"], cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["metric"] == json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 3
+    assert d["unit"] == "images/sec" and d["higher_is_better"] is True
+    assert d["scaling"] == "weak" and d["dtype"] == "bf16" and d["data"].startswith("synthetic")
+    assert d["config"]["model"] == "mnist_cnn" and d["config"]["parallelism"] == "dp1"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # value is the whole-job images/sec implied by the timed steps
+    assert abs(d["value"] - d["config"]["global_batch"] / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
+    assert d["vs_baseline"] > 1.0
