@@ -286,16 +286,23 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
 #pragma unroll
     for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
   if (threadIdx.x == 0) PDM_STAMP_VAL(11, PDM_CLOCK());
-  // clear dz2 while the loads are in flight: the whole padded image for the first image
-  // (the border is never written), the interior for later ones (previous scatter)
+  // First image of the workgroup: zero the 2-pixel border of the padded dz2 image (never
+  // written afterwards) while the loads are in flight.  The 24x24 interior needs no
+  // clearing: the window writes below cover every interior pixel exactly once.
   if (first) {
-    for (int i = tid; i < DZW * DZW * 8; i += BWD_THREADS)
-      *reinterpret_cast<uint4*>(dzs + i * 16) = make_uint4(0, 0, 0, 0);
-  } else {
-    for (int i = tid; i < P2 * 8; i += BWD_THREADS) {
-      const int pix = i >> 3, r = pix / H2, c = pix - r * H2;
-      *reinterpret_cast<uint4*>(dzs + ((r + 2) * DZW + c + 2) * 128 + (i & 7) * 16) =
-          make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < 208 * 8; i += BWD_THREADS) {
+      const int pix = i >> 3;
+      int r, c;
+      if (pix < 112) {                    // rows 0, 1, 26, 27
+        r = pix / DZW;
+        c = pix - r * DZW;
+        r = r < 2 ? r : r + 24;
+      } else {                            // columns 0, 1, 26, 27 of rows 2..25
+        const int q = pix - 112;
+        r = 2 + (q >> 2);
+        c = (q & 3) < 2 ? (q & 3) : (q & 3) + 24;
+      }
+      *reinterpret_cast<uint4*>(dzs + (r * DZW + c) * 128 + (i & 7) * 16) = make_uint4(0, 0, 0, 0);
     }
   }
   if (tid < 196) {
@@ -305,10 +312,11 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   } else if (tid < 200) {
     reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};
   }
-  __syncthreads();
-  // scatter: each pooled gradient goes to its window's argmax pixel (if it was > 0);
-  // dz2 is zero everywhere else.  For window pos s = 2dy + dx the padded pixel is
-  // base + (dy*28 + dx) and its chunk swizzle (2r + c) & 7 is (b0 + s) & 7.
+  // maxpool backward as whole-window writes: item (pooled pixel pp, 8-channel chunk ch)
+  // builds the 16-B chunk of each of the window's 4 pixels (the pooled gradient at the
+  // channel's argmax position if it was > 0, zero elsewhere) and stores 4 x 16 B.
+  // For window pos s = 2dy + dx the padded pixel is base + (dy*28 + dx) and its chunk
+  // swizzle (2r + c) & 7 is (b0 + s) & 7.
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int it = tid + k * BWD_THREADS;   // it & 7 == tid & 7: fixed channel chunk
@@ -319,17 +327,26 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
       const int b0 = 4 * py + 2 * px + 6;
       const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
       const uint32_t mw[2] = {mk[k].x, mk[k].y};
+      uint32_t sel[8];                       // per channel: window position, or 4 if <= 0
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t mb = (mw[j >> 2] >> (8 * (j & 3))) & 0xff;
         const uint32_t dv = (dw[j >> 1] >> (16 * (j & 1))) & 0xffff;
-        // branch-free: a non-positive window writes 0 to its (already zero) argmax pixel
-        const uint32_t dm = (mb & 0x80) ? dv : 0u;
-        db2p[j] += __builtin_bit_cast(float, dm << 16);
-        const int sw = mb & 3;
-        const int off = base + (sw >> 1) * (DZW * 128) + (sw & 1) * 128 +
-                        ((ch ^ ((b0 + sw) & 7)) << 4) + 2 * j;
-        *reinterpret_cast<uint16_t*>(dzs + off) = (uint16_t)dm;
+        sel[j] = (mb & 0x80) ? (mb & 3) : 4u;
+        db2p[j] += __builtin_bit_cast(float, ((mb & 0x80) ? dv : 0u) << 16);
+      }
+#pragma unroll
+      for (int sw = 0; sw < 4; ++sw) {
+        uint4 o;
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t w = dw[q];
+          ow[q] = (sel[2 * q] == (uint32_t)sw ? (w & 0xffffu) : 0u) |
+                  (sel[2 * q + 1] == (uint32_t)sw ? (w & 0xffff0000u) : 0u);
+        }
+        const int off = base + (sw >> 1) * (DZW * 128) + (sw & 1) * 128 + ((ch ^ ((b0 + sw) & 7)) << 4);
+        *reinterpret_cast<uint4*>(dzs + off) = o;
       }
     }
   }
