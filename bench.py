@@ -117,8 +117,7 @@ def main():
     run(a.warmup)
 
     def barrier():
-        if ws > 1:
-            torch.distributed.barrier()
+        parallel.control_barrier()      # gloo (CPU tensor): no torch NCCL communicator
 
     torch.cuda.synchronize()
     barrier()

@@ -32,6 +32,9 @@ for which, names in (("fwd", ["start", "gathered(barrier)", "conv1(barrier)", "c
         print(f"   {nm:22s} {med[i]:9.0f} {mx[i]:9.0f}")
     print("   block start skew (cycles):", (st[:, 0] - t0).max().item(),
           " last end:", (st[:, n - 1] - t0).max().item())
+    if which == "fwd":
+        print("   image load issued (rel)", (st[:, 8] - st[:, 0]).median().item(),
+              " image landed (rel)", (st[:, 9] - st[:, 0]).median().item())
     if which == "bwd":
         print("   dgrad wave4: mfma-section cycles", st[:, 8].median().item(),
               " epilogue cycles", st[:, 9].median().item(),
