@@ -37,11 +37,16 @@ best_acc = 0
 
 
 def _printer(rank, prefix):
-    def p(*a, **k):
+    """print() semantics (space-joined args), but each line reaches stdout in ONE write, so
+    the lines of concurrently printing ranks never interleave mid-line."""
+    import sys
+
+    def p(*a, sep=" ", end="\n"):
+        line = sep.join(str(x) for x in a)
         if prefix:
-            print("[rank {}]".format(rank), *a, **k, flush=True)
-        else:
-            print(*a, **k, flush=True)
+            line = "[rank {}] ".format(rank) + line
+        sys.stdout.write(line + end)
+        sys.stdout.flush()
     return p
 
 

@@ -50,6 +50,11 @@ def pick_device(local_rank: int, want: str = "auto") -> torch.device:
         return torch.device("cpu")
     if want in ("auto", "cuda") and torch.cuda.is_available():
         n = torch.cuda.device_count()
+        if os.environ.get("PDM_SHARE_DEVICE") == "1":
+            # test rehearsal only: every rank on device 0 (gloo data plane; RCCL refuses
+            # two ranks on one GPU) to exercise the multi-rank GPU program on a 1-GPU box
+            torch.cuda.set_device(0)
+            return torch.device("cuda", 0)
         if local_rank >= n:
             raise RuntimeError(f"local rank {local_rank} has no GPU (device_count={n})")
         torch.cuda.set_device(local_rank)
