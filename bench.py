@@ -71,7 +71,10 @@ def main():
     from types import SimpleNamespace
 
     device = parallel.pick_device(local_rank, "cuda")
-    ctx = parallel.init_distributed("nccl", "env://" if ws > 1 else None, ws, rank, local_rank,
+    # PDM_BENCH_BACKEND=gloo: rehearsal of the multi-rank flow on a single GPU (with
+    # PDM_SHARE_DEVICE=1); the measured configuration is always nccl = RCCL
+    backend = os.environ.get("PDM_BENCH_BACKEND", "nccl")
+    ctx = parallel.init_distributed(backend, "env://" if ws > 1 else None, ws, rank, local_rank,
                                     device, init_pg=ws > 1)
     comm = parallel.make_comm(ctx)
     model = a.model

@@ -27,3 +27,21 @@ def test_bench_json_contract(gpu):
     # value is the whole-job images/sec implied by the timed steps
     assert abs(d["value"] - d["config"]["global_batch"] / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
     assert d["vs_baseline"] > 1.0
+
+
+def test_bench_two_rank_flow_rehearsal(gpu):
+    """The N>1 driver path (torch.distributed.run, env rendezvous, barrier + max over ranks,
+    rank-0 JSON) rehearsed with 2 ranks on one GPU over a gloo data plane."""
+    from conftest import free_port
+    env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--steps", "10", "--warmup", "2"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 2 * d["config"]["batch_per_rank"]
