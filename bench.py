@@ -76,7 +76,10 @@ def main():
     backend = os.environ.get("PDM_BENCH_BACKEND", "nccl")
     ctx = parallel.init_distributed(backend, "env://" if ws > 1 else None, ws, rank, local_rank,
                                     device, init_pg=ws > 1)
-    comm = parallel.make_comm(ctx)
+    # PDM_FORCE_COMM=1 at N=1: run the multi-GPU step structure (unfused conv reduction,
+    # grouped RCCL all-reduce through a 1-rank communicator) to price it without transfers
+    force_comm = os.environ.get("PDM_FORCE_COMM") == "1"
+    comm = parallel.make_comm(ctx, force_native=force_comm)
     model = a.model
     dtype = "bf16" if model == "cnn" else "fp32"
     optname = a.optimizer or ("sgd" if model == "cnn" else "adam")
@@ -88,7 +91,7 @@ def main():
     arena.load_module(MODULES[model]())
     comm.broadcast_(arena.params, 0)
     opt = build_optimizer(optname, arena, SimpleNamespace(lr=lr, momentum=0.9, weight_decay=1e-4))
-    reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds())
+    reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds(), force=force_comm)
     train = synthetic_split(a.train_size, True)
     test = synthetic_split(1024, False)
     B = a.batch_per_rank

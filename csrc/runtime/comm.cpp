@@ -191,6 +191,20 @@ class GradReducer {
     pending_ = true;
   }
 
+  // every bucket in one RCCL group (a single collective launch), ordered after the
+  // caller's current stream
+  void all_ready() {
+    hipStream_t cur = comm_.caller();
+    HIP_OK(hipEventRecord(ready_[0], cur));
+    HIP_OK(hipStreamWaitEvent(comm_.stream(), ready_[0], 0));
+    NCCL_OK(ncclGroupStart());
+    for (size_t i = 0; i < starts_.size(); ++i)
+      comm_.all_reduce_range(grads_.data_ptr<float>() + starts_[i], (size_t)counts_[i], ncclFloat32);
+    NCCL_OK(ncclGroupEnd());
+    for (auto& e : reduced_) HIP_OK(hipEventRecord(e, comm_.stream()));
+    pending_ = true;
+  }
+
   // make the caller's current stream wait for bucket i's all-reduce only (e.g. a side
   // stream running that bucket's optimizer while later backward kernels still run)
   void wait_bucket(int i) {
@@ -240,5 +254,6 @@ void register_comm(py::module& m) {
       .def("bucket_ready", &GradReducer::bucket_ready)
       .def("finalize", &GradReducer::finalize)
       .def("wait_bucket", &GradReducer::wait_bucket)
+      .def("all_ready", &GradReducer::all_ready)
       .def_property_readonly("num_buckets", &GradReducer::num_buckets);
 }

@@ -60,6 +60,16 @@ class GradReducer:
         else:
             self.comm.all_reduce_(view)
 
+    def all_ready(self) -> None:
+        """Every bucket is complete: all-reduce them together (one grouped RCCL launch)."""
+        if not self.active:
+            return
+        if self._native is not None:
+            self._native.all_ready()
+            return
+        for i in range(len(self.bounds)):
+            self.bucket_ready(i)
+
     def wait_bucket(self, i: int) -> None:
         """Make the current stream (or the host, on the torch path) wait for bucket i only."""
         if not self.active:

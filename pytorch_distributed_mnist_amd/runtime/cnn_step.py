@@ -183,7 +183,17 @@ class CnnStep(GpuStepBase):
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view())
-        self.reducer.bucket_ready(0)
+        # Bucket 0 (fc, 4.7 MB) is complete here, but RCCL's all-reduce kernel cannot run
+        # next to cnn_bwd: it needs 19.7 KB LDS + ~280 registers per lane (gfx950 code
+        # object metadata of torch's librccl), while cnn_bwd leaves 5.6 KB LDS and 48
+        # registers per SIMD lane on every CU.  Issued here it would either wait for
+        # cnn_bwd anyway or, on its high-priority queue, take CUs first and push part of
+        # cnn_bwd into a second round.  So on the RCCL path both buckets are reduced
+        # together after conv_reduce (one grouped launch); the split path keeps the
+        # per-bucket overlap for the experiment.
+        overlap_b0 = self.split_opt or not getattr(self.reducer, "_native", None)
+        if overlap_b0:
+            self.reducer.bucket_ready(0)
         if self.split_opt:
             # bucket 0's update on the side stream, overlapping cnn_bwd / conv_reduce
             b0, b1 = self._bucket_segments()
@@ -200,7 +210,10 @@ class CnnStep(GpuStepBase):
             return
         C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
-        self.reducer.bucket_ready(1)
+        if overlap_b0:
+            self.reducer.bucket_ready(1)
+        else:
+            self.reducer.all_ready()
         if self.split_opt:
             self.reducer.wait_bucket(1)
             self.launch_optimizer(b1)
