@@ -1,18 +1,22 @@
 """CNN (bf16) GPU step program.
 
-Kernel chain of one training step (all on the compute stream; the two bucket
-all-reduces fork onto the RCCL stream):
+Kernel chain of one training step (compute stream; all-reduces on the RCCL stream):
 
   cnn_fwd      gather+normalise, conv1+ReLU, conv2+ReLU+maxpool  -> pool, mask, x
   fc1_fwd      split-K fc1 GEMM                                  -> fp32 partials
   cnn_head     fc1 reduce+bias+ReLU, fc2, CE, head backward      -> dh, dh^T, head slabs
                (advances the data-step and optimizer-step counters)
-  fc1_bwd      dW1 tiles | dX tiles | head-slab reduce           -> bucket 0 complete
-  [all-reduce bucket 0 on the comm stream, overlapping the next two kernels]
+  fc1_bwd      dW1 tiles | dX tiles | head-slab reduce           -> bucket 0 (fc) complete
   cnn_bwd      a1 recompute, conv2 wgrad | conv2 dgrad + conv1 wgrad -> conv slabs
-  conv_reduce  fixed-order slab sum                              -> bucket 1 complete
-  [all-reduce bucket 1]
-  optim        SGD/Adam over the arena + bf16 weight copies (W1, W1^T, W2, W2^T)
+
+  world_size 1:
+  optim        conv slab reduction fused in; SGD/Adam over the arena + bf16 weight copies
+  world_size > 1:
+  conv_reduce  fixed-order slab sum                              -> bucket 1 (conv) complete
+  [all-reduce bucket 1, then bucket 0]
+  optim(conv)  after bucket 1
+  optim(fc)    after bucket 0 -- inside a multi-step graph deferred to after the next
+               step's cnn_fwd, which overlaps the 4.7 MB fc all-reduce
 
 Evaluation runs cnn_fwd (no activations kept) -> fc1_fwd -> cnn_head over the
 whole test set in chunks of EVAL_CHUNK images.
@@ -81,16 +85,11 @@ class CnnStep(GpuStepBase):
                                     "fc2.weight", "fc2.bias")}
         self.G = {n: g(n) for n in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias",
                                     "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")}
-        # Experiment knob (PDM_SPLIT_OPT=1): run the fc-bucket optimizer on a side stream,
-        # concurrent with the conv backward.  Measured on MI355X at B=256 it is slower
-        # (90.6 vs 74.7 us/step: its workgroups take CUs ahead of cnn_bwd), so it is off.
-        self.split_opt = os.environ.get("PDM_SPLIT_OPT", "0") == "1"
         # world_size 1 (no all-reduce between backward and update): the conv gradient
         # reduction is fused into the optimizer launch (PDM_FUSE_CONV_REDUCE=0 disables)
-        self.fuse_conv_reduce = (not self.reducer.active and not self.split_opt and
+        self.fuse_conv_reduce = (not self.reducer.active and
                                  os.environ.get("PDM_FUSE_CONV_REDUCE", "1") != "0")
         self._fused = {}
-        self.side = torch.cuda.Stream(device=dev)
         self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
         self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
         self.refresh_shadows()
@@ -169,13 +168,30 @@ class CnnStep(GpuStepBase):
             self._fused[nblk] = segs
         return segs
 
-    def _train_impl(self, B: int) -> None:
+    def _train_seq(self, B: int, n: int) -> None:
+        # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
+        # runs while the fc gradients are still being all-reduced; the last step of the
+        # sequence (a graph must rejoin the comm stream) does not carry
+        carry = self.reducer.active and getattr(self.reducer, "_native", None) is not None
+        for i in range(n):
+            self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
+
+    def _train_impl(self, B: int, carry_in: bool = False, carry_out: bool = False) -> None:
+        """One training step (kernel chain in the module docstring).
+
+        carry_in: the previous step's fc-bucket optimizer update is still pending; it runs
+        after this step's cnn_fwd (which only needs the conv weights), so the previous fc
+        all-reduce overlaps cnn_fwd.  carry_out: leave this step's fc update to the next step.
+        """
         C, P, G = self.C, self.P, self.G
         ldt = -(-B // 32) * 32
         S = self.splitk_train
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
                   self.pmask, self.xg, self.ylab)
+        if carry_in:
+            self.reducer.wait_bucket(0)
+            self.launch_optimizer(self._bucket_segments()[0])
         C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
         C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab, True,
                    self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
@@ -183,44 +199,37 @@ class CnnStep(GpuStepBase):
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view())
-        # Bucket 0 (fc, 4.7 MB) is complete here, but RCCL's all-reduce kernel cannot run
-        # next to cnn_bwd: it needs 19.7 KB LDS + ~280 registers per lane (gfx950 code
-        # object metadata of torch's librccl), while cnn_bwd leaves 5.6 KB LDS and 48
-        # registers per SIMD lane on every CU.  Issued here it would either wait for
-        # cnn_bwd anyway or, on its high-priority queue, take CUs first and push part of
-        # cnn_bwd into a second round.  So on the RCCL path both buckets are reduced
-        # together after conv_reduce (one grouped launch); the split path keeps the
-        # per-bucket overlap for the experiment.
-        overlap_b0 = self.split_opt or not getattr(self.reducer, "_native", None)
-        if overlap_b0:
-            self.reducer.bucket_ready(0)
-        if self.split_opt:
-            # bucket 0's update on the side stream, overlapping cnn_bwd / conv_reduce
-            b0, b1 = self._bucket_segments()
-            cur = torch.cuda.current_stream(self.device)
-            self.side.wait_stream(cur)
-            with torch.cuda.stream(self.side):
-                self.reducer.wait_bucket(0)
-                self.launch_optimizer(b0)
         ipb = choose_ipb(B)
         C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
                   ipb, self.conv_slab)
         if self.fuse_conv_reduce:
+            # world_size 1: no all-reduce, the conv slab reduction runs inside the update
             self.launch_optimizer(self._fused_segments(C.cnn_bwd_nblk(B, ipb)))
             return
         C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
-        if overlap_b0:
+        if getattr(self.reducer, "_native", None) is None:
+            # gloo data plane (rehearsal / CPU-staged): plain bucket order, one update
+            self.reducer.bucket_ready(0)
             self.reducer.bucket_ready(1)
-        else:
-            self.reducer.all_ready()
-        if self.split_opt:
-            self.reducer.wait_bucket(1)
-            self.launch_optimizer(b1)
-            cur.wait_stream(self.side)
-        else:
             self.reducer.finalize()
             self.launch_optimizer()
+            return
+        # RCCL.  Both buckets are reduced after conv_reduce: RCCL's all-reduce kernel cannot
+        # be co-resident with cnn_bwd (it needs 19.7 KB LDS + ~280 registers per lane per the
+        # gfx950 code-object metadata of torch's librccl; cnn_bwd leaves 5.6 KB LDS and 48
+        # registers per SIMD lane on every CU), so issuing bucket 0 earlier would only wait
+        # for cnn_bwd or push part of it into a second round.  The small conv bucket goes
+        # first (the next forward needs it); the 4.7 MB fc bucket keeps reducing while the
+        # conv update and the next step's cnn_fwd run.
+        b0, b1 = self._bucket_segments()
+        self.reducer.bucket_ready(1)
+        self.reducer.bucket_ready(0)
+        self.reducer.wait_bucket(1)
+        self.launch_optimizer(b1)
+        if not carry_out:
+            self.reducer.wait_bucket(0)
+            self.launch_optimizer(b0)
 
     def evaluate(self) -> None:
         C, P = self.C, self.P

@@ -101,8 +101,7 @@ class GpuStepBase:
         if g is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):          # captured on a side stream
-                for _ in range(nsteps):
-                    self._train_impl(B)
+                self._train_seq(B, nsteps)
             self.graphs[key] = g
         return g
 
@@ -121,12 +120,16 @@ class GpuStepBase:
                 for _ in range(n % k):
                     g1.replay()
         else:
-            for _ in range(n):
-                self._train_impl(B)
+            self._train_seq(B, n)
         self.opt.step_count += n
 
     def train_step(self, B: int) -> None:
         self.train_steps(B, 1)
+
+    def _train_seq(self, B: int, n: int) -> None:
+        """n consecutive steps (captured together into one graph, or eager)."""
+        for _ in range(n):
+            self._train_impl(B)
 
     def _train_impl(self, B: int) -> None:
         raise NotImplementedError
