@@ -91,11 +91,28 @@ def main():
     arena.load_module(MODULES[model]())
     comm.broadcast_(arena.params, 0)
     opt = build_optimizer(optname, arena, SimpleNamespace(lr=lr, momentum=0.9, weight_decay=1e-4))
-    reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds(), force=force_comm)
+    bounds = spec.bucket_bounds()
+    # Gradient transports to choose from: with $PDM_COMM unset (auto) on the RCCL data plane
+    # both the direct xGMI all-reduce and RCCL are built, and a short untimed calibration
+    # run of the real step picks the faster one for this N (agreed over ranks).
+    want = os.environ.get("PDM_COMM", "auto")
+    reducers = {}
+    if (ws > 1 or force_comm) and want == "auto" and isinstance(comm, parallel.RcclComm):
+        try:
+            reducers["xgmi"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
+                                                    transport="xgmi")
+        except Exception as e:                # collective decision: no rank uses xgmi
+            print(f"bench.py: xgmi transport unavailable: {e}", file=sys.stderr, flush=True)
+        reducers["rccl"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
+                                                transport="rccl")
+    else:
+        r0 = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm, transport=want)
+        reducers[r0.kind] = r0
     train = synthetic_split(a.train_size, True)
     test = synthetic_split(1024, False)
     B = a.batch_per_rank
-    prog = TrainProgram(model, dtype, arena, opt, reducer, train, test, B, use_graphs=a.graphs)
+    first = next(iter(reducers.values()))
+    prog = TrainProgram(model, dtype, arena, opt, first, train, test, B, use_graphs=a.graphs)
     n = len(train)
 
     state = {"epoch": 0, "step": 0}
@@ -118,26 +135,46 @@ def main():
             state["step"] += m
             k -= m
 
-    opt.sync_hyperparams()
-    next_epoch()
-    run(a.warmup)
-
     def barrier():
         parallel.control_barrier()      # gloo (CPU tensor): no torch NCCL communicator
 
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(a.steps)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(k):
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(k)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if ws > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    def use(red):
+        prog.reducer = red
+        prog.gpu.reducer = red
+        prog.gpu.use_graphs = bool(a.graphs) and red.capturable
+        prog.gpu.invalidate_graphs()
+
+    opt.sync_hyperparams()
+    next_epoch()
+    calib = {}
+    if len(reducers) > 1:
+        for name, red in reducers.items():
+            use(red)
+            run(16)
+            calib[name] = timed(48) / 48 * 1e3
+            red.check()
+        best = min(calib, key=calib.get)
+        use(reducers[best])
+    chosen = prog.reducer
+    run(a.warmup)
+    elapsed = timed(a.steps)
+    chosen.check()
     if not torch.isfinite(arena.params).all():
         raise RuntimeError("non-finite parameters after the benchmark")
     ms = elapsed / a.steps * 1e3
@@ -156,8 +193,12 @@ def main():
             "config": {"model": "mnist_cnn" if model == "cnn" else "mnist_linear",
                        "global_batch": global_batch, "batch_per_rank": B, "seq_len": None,
                        "parallelism": f"dp{ws}", "optimizer": optname,
-                       "graphs": bool(prog.gpu.use_graphs)},
+                       "graphs": bool(prog.gpu.use_graphs), "grad_transport": chosen.kind,
+                       "transport_calibration_ms_per_step":
+                           {k: round(v, 5) for k, v in calib.items()}},
         }), flush=True)
+    for red in reducers.values():
+        red.close()
     comm.close()
     parallel.shutdown()
 

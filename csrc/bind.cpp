@@ -9,6 +9,7 @@
 
 namespace py = pybind11;
 void register_comm(py::module& m);
+void register_xgmi(py::module& m);
 
 namespace {
 
@@ -414,4 +415,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk);
   m.def("read_stamps", &read_stamps);
   register_comm(m);
+  register_xgmi(m);
 }

@@ -1,0 +1,173 @@
+// Direct xGMI all-reduce kernel (protocol: csrc/xgmi.h).
+//
+// Why not RCCL for the 4.7 MB fc bucket: RCCL's all-reduce kernel needs 19.7 KB
+// of LDS and ~280 registers per lane (docs/kernels.md), so it cannot share a CU
+// with cnn_bwd and the fc gradients can only travel after the whole backward.
+// This kernel uses one LDS word and at most 48 registers per lane (waves_per_eu
+// 10), which fits in what cnn_bwd leaves free on every CU, so it runs *beside*
+// cnn_bwd; and its push schedule moves the bucket over all N-1 point-to-point
+// links at once instead of one link per ring step.
+//
+// Memory-model recipe (system scope, gfx950):
+//   payload  16-B buffer stores with sc0 sc1 (write-through to the owning HBM),
+//            each storing wave drains them (s_waitcnt vmcnt(0)), workgroup barrier;
+//   signal   one relaxed system-scope store of the call generation per peer flag;
+//   consume  one wave polls its peers' flags (relaxed system-scope loads, s_sleep),
+//            then a system-scope acquire (buffer_inv sc0 sc1) and a barrier before
+//            any wave loads the handed-off bytes.
+// All hand-off memory is uncached (hipDeviceMallocUncached), so no L2 on either
+// side can hold a stale copy across calls.  Every spin is bounded: past
+// `timeout` ticks the workgroup records the phase in `err` and exits, so a dead
+// peer turns into a host-visible error instead of a hung GPU.
+#include "common.h"
+#include "xgmi.h"
+
+namespace {
+
+constexpr int XG_SC0_SC1 = 17;              // aux bits of a system-scope write-through store
+constexpr int XG_RSRC_W3 = 0x00020000;      // raw buffer descriptor word 3 (gfx9 family)
+constexpr int XG_BATCH = 4;                 // loads kept in flight per lane before their use
+
+__device__ __forceinline__ unsigned flag_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void flag_store(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, XG_RSRC_W3);
+}
+
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, long long i4, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(i4 * 16), 0, XG_SC0_SC1);
+}
+
+__device__ __forceinline__ long long clampll(long long v, long long lo, long long hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// Every storing wave drains its write-through stores, then one lane publishes the
+// generation into each peer's flag block.
+__device__ __forceinline__ void signal_peers(const XgmiArgs& a, int ph, int w, unsigned gen) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int d = 0; d < a.nranks; ++d)
+      if (d != a.rank) flag_store(a.flags[d] + xg_flag_idx(a.ch, ph, a.rank, w), gen);
+  }
+}
+
+// Wave 0 polls this rank's flags from every peer until each reaches `gen` (or the
+// deadline passes), then acquires; the verdict reaches every wave through LDS.
+__device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, unsigned gen,
+                                           long long deadline, int* s_ok) {
+  if (threadIdx.x < PDM_WAVE) {
+    const int lane = threadIdx.x;
+    const bool mine = lane < a.nranks && lane != a.rank;
+    const unsigned* f = a.flags[a.rank] + xg_flag_idx(a.ch, ph, mine ? lane : 0, w);
+    bool ok = true;
+    for (;;) {
+      const bool arrived = !mine || (int)(flag_load(f) - gen) >= 0;
+      if (__all(arrived)) break;
+      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // buffer_inv sc0 sc1
+    if (lane == 0) {
+      *s_ok = ok;
+      if (!ok) atomicOr(a.err, 1u << ph);
+    }
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+__global__ __launch_bounds__(XG_THREADS) __attribute__((amdgpu_waves_per_eu(10, 10)))
+void xgmi_allreduce_kernel(XgmiArgs a) {
+  __shared__ int s_ok;
+  const int w = blockIdx.x, W = gridDim.x, tid = threadIdx.x;
+  const int N = a.nranks, r = a.rank;
+  const unsigned gen = a.gen[w] + 1;   // this workgroup's call count on this channel
+  const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
+  const f32x4* src = reinterpret_cast<const f32x4*>(a.src);
+  const long long n4 = a.n >> 2;
+  const bool two = a.mode == XG_TWO_SHOT;
+  // two-shot: chunk d of the bucket belongs to rank d; one-shot: one "chunk" = the bucket
+  const long long c4 = two ? (a.chunk >> 2) : n4;
+  const long long per = (c4 + W - 1) / W;               // float4 per workgroup slice
+  const long long lo = (long long)w * per;
+  const long long par = two ? 0 : (gen & 1u);           // one-shot stage double buffer
+  const long long row4 = c4;                            // stage row length (float4)
+
+  // phase 0: push slice w of chunk d (two-shot) / of the bucket (one-shot) into row r
+  // of rank d's stage.  Workgroups start at different peers so all N-1 links carry
+  // traffic at once; XG_BATCH loads are issued before their stores.
+  for (int i0 = 0; i0 < N - 1; i0 += XG_BATCH) {
+    int dd[XG_BATCH];
+    long long hid[XG_BATCH];
+#pragma unroll
+    for (int b = 0; b < XG_BATCH; ++b) {
+      const int i = i0 + b < N - 1 ? i0 + b : i0;
+      dd[b] = (r + 1 + (i + w) % (N - 1)) % N;
+      const long long len = two ? clampll(n4 - (long long)dd[b] * c4, 0, c4) : n4;
+      hid[b] = i0 + b < N - 1 ? (lo + per < len ? lo + per : len) : 0;
+    }
+    for (long long j = lo + tid; j < lo + per; j += XG_THREADS) {
+      f32x4 v[XG_BATCH];
+#pragma unroll
+      for (int b = 0; b < XG_BATCH; ++b)
+        if (j < hid[b]) v[b] = src[(two ? (long long)dd[b] * c4 : 0) + j];
+#pragma unroll
+      for (int b = 0; b < XG_BATCH; ++b)
+        if (j < hid[b]) store_wt(rsrc(a.stage[dd[b]] + (par * N + r) * row4 * 4), j, v[b]);
+    }
+  }
+  signal_peers(a, 0, w, gen);
+  if (!wait_peers(a, 0, w, gen, deadline, &s_ok)) return;
+
+  // fixed rank-order sum of this rank's chunk (two-shot) / of the whole bucket (one-shot)
+  {
+    const long long base = two ? (long long)r * c4 : 0;
+    const long long len = two ? clampll(n4 - base, 0, c4) : n4;
+    const long long hi = lo + per < len ? lo + per : len;
+    const f32x4* own = src + base;
+    const f32x4* stage = reinterpret_cast<const f32x4*>(a.stage[r]) + par * N * row4;
+    const long long res = a.off + base * 4;             // float offset in the result arena
+    for (long long j = lo + tid; j < hi; j += XG_THREADS) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < N; s0 += XG_BATCH) {
+        f32x4 v[XG_BATCH];
+#pragma unroll
+        for (int b = 0; b < XG_BATCH; ++b) {
+          const int s = s0 + b;
+          if (s < N) v[b] = s == r ? own[j] : stage[(long long)s * row4 + j];
+        }
+#pragma unroll
+        for (int b = 0; b < XG_BATCH; ++b)
+          if (s0 + b < N) acc = s0 + b == 0 ? v[b] : acc + v[b];
+      }
+      if (two) {
+        // all-gather push: the sum goes into every rank's result arena
+        for (int i = 0; i < N; ++i) store_wt(rsrc(a.result[(r + i + w) % N] + res), j, acc);
+      } else {
+        store_wt(rsrc(a.result[r] + res), j, acc);
+      }
+    }
+  }
+  if (two) {
+    signal_peers(a, 1, w, gen);
+    if (!wait_peers(a, 1, w, gen, deadline, &s_ok)) return;
+  }
+  if (tid == 0) a.gen[w] = gen;
+}
+
+}  // namespace
+
+void launch_xgmi_allreduce(const XgmiArgs& a, int nblk, hipStream_t st) {
+  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nblk), dim3(XG_THREADS), 0, st, a);
+}

@@ -1,0 +1,329 @@
+// Host side of the direct xGMI gradient all-reduce (kernel + protocol: csrc/xgmi.h,
+// csrc/kernels/xgmi.hip).  Replaces the RCCL data plane for the gradient buckets;
+// the RCCL communicator stays for the parameter broadcast and as the fallback.
+//
+// XgmiReducer — one rank's end:
+//   * one uncached device allocation (flags | result arena | per-bucket stage),
+//     exported with hipIpcGetMemHandle; the peers' allocations are mapped with
+//     hipIpcOpenMemHandle (dmabuf), so a kernel addresses every rank's buffers;
+//   * one channel per gradient bucket: one-shot (whole bucket to every peer) for
+//     small buckets or two ranks, two-shot (reduce-scatter + all-gather push) for
+//     the 4.7 MB fc bucket at 4 and 8 ranks;
+//   * the GradReducer stream protocol (bucket_ready / all_ready / wait_bucket /
+//     finalize): each bucket's kernel runs on a high-priority stream behind an
+//     event recorded on the caller's stream, so the whole exchange is captured in
+//     the step's hipGraph and overlaps whatever the compute stream runs next.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "xgmi.h"
+
+namespace py = pybind11;
+
+#define XG_HIP_OK(x)                                                                      \
+  do {                                                                                    \
+    hipError_t _e = (x);                                                                  \
+    TORCH_CHECK(_e == hipSuccess, "HIP error ", hipGetErrorString(_e), " at ", #x);       \
+  } while (0)
+
+namespace {
+
+constexpr size_t kAlign = 1 << 16;
+constexpr int64_t kOneShotMaxBytes = 256 << 10;   // buckets up to this size go one-shot
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Process-wide registry of exported heaps and opened peer mappings.  A heap is
+// exported once and reused by later reducers of the process (re-zeroed), and a
+// peer's handle is opened once: freeing an exported allocation and allocating a
+// new one let hipIpcGetMemHandle fail with "invalid argument" on ROCm 7.0, and a
+// re-opened handle of a recycled address could map the old pages.
+struct Heap {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  bool in_use = false;
+  bool exported = false;
+  hipIpcMemHandle_t handle;
+};
+std::mutex g_mu;
+std::map<int, std::vector<Heap*>> g_heaps;          // device -> heaps (never freed)
+std::map<std::string, void*> g_peer_maps;            // handle bytes -> local mapping
+
+Heap* acquire_heap(int device, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (Heap* h : g_heaps[device])
+    if (!h->in_use && h->bytes >= bytes) {
+      h->in_use = true;
+      return h;
+    }
+  Heap* h = new Heap();
+  XG_HIP_OK(hipExtMallocWithFlags(&h->ptr, bytes, hipDeviceMallocUncached));
+  h->bytes = bytes;
+  h->in_use = true;
+  g_heaps[device].push_back(h);
+  return h;
+}
+
+void* open_peer(const std::string& key) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_peer_maps.find(key);
+  if (it != g_peer_maps.end()) return it->second;
+  hipIpcMemHandle_t h;
+  memcpy(&h, key.data(), sizeof(h));
+  void* p = nullptr;
+  XG_HIP_OK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  g_peer_maps[key] = p;
+  return p;
+}
+
+struct Channel {
+  int64_t start, n, chunk;
+  int mode, nblk;
+  size_t stage_off;   // byte offset of this channel's stage area in the heap
+};
+
+}  // namespace
+
+class XgmiReducer {
+ public:
+  XgmiReducer(int rank, int nranks, int device, at::Tensor grads, std::vector<int64_t> bounds,
+              double timeout_s, std::string mode)
+      : rank_(rank), nranks_(nranks), device_(device), grads_(grads) {
+    TORCH_CHECK(nranks >= 1 && nranks <= XG_MAX_RANKS, "xgmi all-reduce supports 1..",
+                XG_MAX_RANKS, " ranks, got ", nranks);
+    TORCH_CHECK(rank >= 0 && rank < nranks, "bad rank");
+    TORCH_CHECK(grads.is_cuda() && grads.get_device() == device, "grads must live on device ", device);
+    TORCH_CHECK(grads.scalar_type() == at::kFloat && grads.is_contiguous(), "grads must be contiguous fp32");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(grads.data_ptr()) % 256 == 0, "grads must be 256-B aligned");
+    TORCH_CHECK(bounds.size() % 2 == 0 && !bounds.empty() && bounds.size() / 2 <= XG_MAX_CH,
+                "1..", XG_MAX_CH, " buckets as (start, end) pairs");
+    TORCH_CHECK(mode == "auto" || mode == "one" || mode == "two", "mode must be auto|one|two");
+    arena_ = grads.numel();
+    // heap layout: flags | result arena | stage of channel 0 | stage of channel 1 | ...
+    size_t off = round_up((size_t)XG_FLAG_WORDS * 4, kAlign);
+    result_off_ = off;
+    off += round_up((size_t)arena_ * 4, kAlign);
+    for (size_t i = 0; i < bounds.size(); i += 2) {
+      Channel c;
+      c.start = bounds[i];
+      c.n = bounds[i + 1] - bounds[i];
+      TORCH_CHECK(c.start >= 0 && c.n > 0 && bounds[i + 1] <= arena_, "bucket out of range");
+      TORCH_CHECK(c.start % 64 == 0 && c.n % 64 == 0, "buckets must be 64-float aligned");
+      bool two = nranks > 2 && c.n * 4 > kOneShotMaxBytes;
+      if (mode == "one") two = false;
+      if (mode == "two") two = nranks > 1;
+      c.mode = two ? XG_TWO_SHOT : XG_ONE_SHOT;
+      c.chunk = two ? (int64_t)round_up((size_t)((c.n + nranks - 1) / nranks), 64) : c.n;
+      const int64_t c4 = c.chunk / 4;
+      c.nblk = (int)std::min<int64_t>(XG_MAX_WG, std::max<int64_t>(1, (c4 + XG_THREADS - 1) / XG_THREADS));
+      c.stage_off = off;
+      const size_t stage_floats = two ? (size_t)nranks * c.chunk : 2 * (size_t)nranks * c.n;
+      TORCH_CHECK(stage_floats * 4 < (size_t)0x7fffffff, "stage area exceeds the 2 GB buffer window");
+      off += round_up(stage_floats * 4, kAlign);
+      ch_.push_back(c);
+    }
+    heap_bytes_ = off;
+    timeout_ticks_ = (long long)(timeout_s * 1e8);   // s_memrealtime runs at 100 MHz
+    XG_HIP_OK(hipSetDevice(device));
+    heap_rec_ = acquire_heap(device, heap_bytes_);
+    heap_ = heap_rec_->ptr;
+    // zeroed before this rank publishes its handle, so no peer can signal into stale flags
+    XG_HIP_OK(hipMemset(heap_, 0, heap_bytes_));
+    XG_HIP_OK(hipMalloc(&local_, (XG_MAX_CH * XG_MAX_WG + 64) * sizeof(unsigned)));
+    XG_HIP_OK(hipMemset(local_, 0, (XG_MAX_CH * XG_MAX_WG + 64) * sizeof(unsigned)));
+    XG_HIP_OK(hipDeviceSynchronize());
+    for (int r = 0; r < XG_MAX_RANKS; ++r) peers_[r] = nullptr;
+    peers_[rank] = heap_;
+    int lo = 0, hi = 0;
+    XG_HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    XG_HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+    ready_.resize(ch_.size());
+    reduced_.resize(ch_.size());
+    for (auto& e : ready_) XG_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : reduced_) XG_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    XG_HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+
+  ~XgmiReducer() { close(); }
+
+  py::bytes ipc_handle() const {
+    alive();
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (!heap_rec_->exported) {
+        XG_HIP_OK(hipIpcGetMemHandle(&heap_rec_->handle, heap_));
+        heap_rec_->exported = true;
+      }
+    }
+    return py::bytes(reinterpret_cast<const char*>(&heap_rec_->handle), sizeof(hipIpcMemHandle_t));
+  }
+
+  // handles[r] = rank r's ipc_handle() (own entry ignored)
+  void open_peers(std::vector<std::string> handles) {
+    alive();
+    TORCH_CHECK((int)handles.size() == nranks_, "need one handle per rank");
+    XG_HIP_OK(hipSetDevice(device_));
+    for (int r = 0; r < nranks_; ++r) {
+      if (r == rank_) continue;
+      TORCH_CHECK(handles[r].size() == sizeof(hipIpcMemHandle_t), "bad ipc handle size");
+      peers_[r] = open_peer(handles[r]);
+    }
+    open_ = true;
+  }
+
+  at::Tensor result() const {
+    alive();
+    auto opts = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_);
+    return torch::from_blob(static_cast<char*>(heap_) + result_off_, {arena_}, [](void*) {}, opts);
+  }
+
+  void bucket_ready(int i) {
+    check_bucket(i);
+    hipStream_t cur = caller();
+    XG_HIP_OK(hipEventRecord(ready_[i], cur));
+    XG_HIP_OK(hipStreamWaitEvent(stream_, ready_[i], 0));
+    launch(i);
+    XG_HIP_OK(hipEventRecord(reduced_[i], stream_));
+    pending_ = true;
+  }
+
+  void all_ready() {
+    TORCH_CHECK(open_ || nranks_ == 1, "open_peers() first");
+    hipStream_t cur = caller();
+    XG_HIP_OK(hipEventRecord(ready_[0], cur));
+    XG_HIP_OK(hipStreamWaitEvent(stream_, ready_[0], 0));
+    for (size_t i = 0; i < ch_.size(); ++i) {
+      launch((int)i);
+      XG_HIP_OK(hipEventRecord(reduced_[i], stream_));
+    }
+    pending_ = true;
+  }
+
+  void wait_bucket(int i) {
+    check_bucket(i);
+    XG_HIP_OK(hipStreamWaitEvent(caller(), reduced_[i], 0));
+  }
+
+  void finalize() {
+    if (!pending_) return;
+    XG_HIP_OK(hipEventRecord(done_, stream_));
+    XG_HIP_OK(hipStreamWaitEvent(caller(), done_, 0));
+    pending_ = false;
+  }
+
+  // error word: bit 0 / 1 = a workgroup gave up waiting for its peers in phase 0 / 1
+  int64_t error() {
+    alive();
+    XG_HIP_OK(hipStreamSynchronize(stream_));
+    unsigned e = 0;
+    XG_HIP_OK(hipMemcpy(&e, err_ptr(), sizeof(e), hipMemcpyDeviceToHost));
+    return e;
+  }
+
+  py::list describe() const {
+    py::list out;
+    for (const auto& c : ch_) {
+      py::dict d;
+      d["start"] = c.start;
+      d["n"] = c.n;
+      d["mode"] = c.mode == XG_TWO_SHOT ? "two-shot" : "one-shot";
+      d["chunk"] = c.chunk;
+      d["blocks"] = c.nblk;
+      out.append(d);
+    }
+    return out;
+  }
+
+  void close() {
+    if (!heap_) return;
+    hipStreamSynchronize(stream_);
+    // peer mappings and the exported heap stay cached for the next reducer (see Heap)
+    for (auto& e : ready_) hipEventDestroy(e);
+    for (auto& e : reduced_) hipEventDestroy(e);
+    hipEventDestroy(done_);
+    hipStreamDestroy(stream_);
+    hipFree(local_);
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      heap_rec_->in_use = false;
+    }
+    heap_ = nullptr;
+    open_ = false;
+  }
+
+  int num_buckets() const { return (int)ch_.size(); }
+
+ private:
+  void alive() const { TORCH_CHECK(heap_ != nullptr, "xgmi reducer closed"); }
+  void check_bucket(int i) const {
+    alive();
+    TORCH_CHECK(i >= 0 && i < (int)ch_.size(), "bad bucket index");
+    TORCH_CHECK(open_ || nranks_ == 1, "open_peers() first");
+  }
+  hipStream_t caller() const { return c10::hip::getCurrentHIPStream(device_).stream(); }
+  unsigned* err_ptr() const { return static_cast<unsigned*>(local_) + XG_MAX_CH * XG_MAX_WG; }
+
+  void launch(int i) {
+    const Channel& c = ch_[i];
+    XgmiArgs a{};
+    for (int r = 0; r < XG_MAX_RANKS; ++r) {
+      char* base = static_cast<char*>(r < nranks_ ? peers_[r] : nullptr);
+      a.stage[r] = base ? reinterpret_cast<float*>(base + c.stage_off) : nullptr;
+      a.result[r] = base ? reinterpret_cast<float*>(base + result_off_) : nullptr;
+      a.flags[r] = base ? reinterpret_cast<unsigned*>(base) : nullptr;
+    }
+    a.src = grads_.data_ptr<float>() + c.start;
+    a.gen = static_cast<unsigned*>(local_) + i * XG_MAX_WG;
+    a.err = err_ptr();
+    a.off = c.start;
+    a.n = c.n;
+    a.chunk = c.chunk;
+    a.timeout = timeout_ticks_;
+    a.rank = rank_;
+    a.nranks = nranks_;
+    a.ch = i;
+    a.mode = c.mode;
+    launch_xgmi_allreduce(a, c.nblk, stream_);
+    XG_HIP_OK(hipGetLastError());
+  }
+
+  int rank_, nranks_, device_;
+  at::Tensor grads_;
+  int64_t arena_ = 0;
+  size_t result_off_ = 0, heap_bytes_ = 0;
+  long long timeout_ticks_ = 0;
+  std::vector<Channel> ch_;
+  Heap* heap_rec_ = nullptr;
+  void* heap_ = nullptr;
+  void* local_ = nullptr;
+  void* peers_[XG_MAX_RANKS];
+  bool open_ = false, pending_ = false;
+  hipStream_t stream_ = nullptr;
+  std::vector<hipEvent_t> ready_, reduced_;
+  hipEvent_t done_ = nullptr;
+};
+
+void register_xgmi(py::module& m) {
+  m.attr("XG_MAX_RANKS") = XG_MAX_RANKS;
+  py::class_<XgmiReducer>(m, "XgmiReducer")
+      .def(py::init<int, int, int, at::Tensor, std::vector<int64_t>, double, std::string>(),
+           py::arg("rank"), py::arg("nranks"), py::arg("device"), py::arg("grads"),
+           py::arg("bounds"), py::arg("timeout_s") = 60.0, py::arg("mode") = "auto")
+      .def("ipc_handle", &XgmiReducer::ipc_handle)
+      .def("open_peers", &XgmiReducer::open_peers)
+      .def("result", &XgmiReducer::result)
+      .def("bucket_ready", &XgmiReducer::bucket_ready)
+      .def("all_ready", &XgmiReducer::all_ready)
+      .def("wait_bucket", &XgmiReducer::wait_bucket)
+      .def("finalize", &XgmiReducer::finalize)
+      .def("error", &XgmiReducer::error)
+      .def("describe", &XgmiReducer::describe)
+      .def("close", &XgmiReducer::close)
+      .def_property_readonly("num_buckets", &XgmiReducer::num_buckets);
+}

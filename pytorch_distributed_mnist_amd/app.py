@@ -137,7 +137,8 @@ def run(args):
     train_split = load_split(args.root, True, synthetic=args.synthetic,
                              synthetic_size=args.synthetic_size)
     test_split = load_split(args.root, False, synthetic=args.synthetic)
-    reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds())
+    reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds(),
+                                   transport=getattr(args, "comm", None))
     dtype = resolve_dtype(args.dtype, args.arch, device)
     program = TrainProgram(args.arch, dtype, arena, optimizer, reducer, train_split, test_split,
                            args.batch_size, use_graphs=args.graphs)
@@ -157,6 +158,7 @@ def run(args):
                 adjust_learning_rate(optimizer, epoch, args)
 
                 train_loss, train_acc = trainer.train()
+                reducer.check()             # xgmi: raise if a peer never arrived
                 test_loss, test_acc = trainer.evaluate()
 
                 out('Epoch: {}/{},'.format(epoch, args.epochs),
@@ -175,6 +177,9 @@ def run(args):
                         save_checkpoint(make_state(epoch + 1, arena, best_acc, optimizer), is_best,
                                         epoch, directory=args.checkpoint_dir)
     finally:
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        reducer.close()
         comm.close()
         parallel.shutdown()
 

@@ -72,6 +72,10 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument('--device', choices=['auto', 'cuda', 'cpu'], default='auto')
     g.add_argument('--no-graphs', dest='graphs', action='store_false',
                    help='launch kernels eagerly instead of replaying captured hipGraphs')
+    g.add_argument('--comm', choices=['auto', 'xgmi', 'rccl'], default=None,
+                   help='gradient all-reduce transport on GPU with --backend nccl: xgmi = direct '
+                        'peer-to-peer pushes over xGMI (hipIpc), rccl = ncclAllReduce; auto '
+                        '(default, or $PDM_COMM) = xgmi when every rank passes its self-check')
     g.add_argument('--checkpoint-dir', default='checkpoints')
     g.add_argument('--timeout', type=float, default=1800.0,
                    help='process-group / rendezvous timeout in seconds')

@@ -2,24 +2,36 @@
 
 Replaces DDP's C++ ``Reducer``.  Gradients already live in
 one flat arena (``runtime/arena.py``) laid out in backward-ready order, so a
-bucket is a contiguous slice and there is nothing to copy in or out:
+bucket is a contiguous slice and there is nothing to copy in:
 
 * the step program calls ``bucket_ready(i)`` right after the kernel that
   finishes bucket i's gradients;
-* on the native path (``RcclComm``) the C++ ``GradReducer`` records an event on
-  the compute stream, makes the comm stream wait on it and enqueues
-  ``ncclAllReduce(sum)`` there — so bucket 0 (fc layers, 4.7 MB for the CNN)
-  travels over xGMI while the conv backward kernel still runs;
+* a native transport records an event on the compute stream, makes its own
+  high-priority stream wait on it and enqueues the bucket's collective there, so
+  it overlaps the kernels the compute stream runs next;
 * ``finalize()`` makes the compute stream wait for every bucket before the
-  optimizer kernel.
+  optimizer kernel, which reads ``out_grads``.
+
+Transports (``transport=``; ``PDM_COMM`` overrides the default ``auto``):
+
+* ``xgmi`` — the direct peer-to-peer all-reduce over xGMI (``csrc/xgmi.h``):
+  the gradients are pushed into the peers' uncached hipIpc-mapped buffers and
+  the sums land in an arena-sized result buffer (``out_grads``).  Its kernel is
+  small enough to run beside ``cnn_bwd``, so the 4.7 MB fc bucket travels during
+  the conv backward.  Sums are in fixed rank order (bit-identical on all ranks).
+* ``rccl`` — ``ncclAllReduce`` on the C++ RCCL communicator, in place.
+* ``auto`` — xgmi when every rank can map its peers and a numerical check of
+  the transport passes on every rank, otherwise rccl (with a warning).
 
 The reference DDP pre-divides by world_size and sums; we sum and fold the
 1/world_size into the optimizer kernel (identical bits for power-of-two world
 sizes).  With world_size 1 no collective is issued unless ``force`` is set
-(the tests force it to exercise the RCCL path on a single GPU).
+(the tests force it to exercise the native transports on a single GPU).
 """
 from __future__ import annotations
 
+import os
+import sys
 from typing import List, Tuple
 
 import torch
@@ -27,21 +39,58 @@ import torch
 from ..ops import _ext
 from .comm import Communicator, RcclComm, TorchComm
 
+TRANSPORTS = ("auto", "xgmi", "rccl")
+
+
+def default_transport() -> str:
+    t = os.environ.get("PDM_COMM", "auto")
+    if t not in TRANSPORTS:
+        raise ValueError(f"PDM_COMM={t!r}: choose from {TRANSPORTS}")
+    return t
+
 
 class GradReducer:
     def __init__(self, comm: Communicator, grads: torch.Tensor, bounds: List[Tuple[int, int]],
-                 force: bool = False):
+                 force: bool = False, transport: str | None = None):
         self.comm = comm
         self.grads = grads
+        self.out_grads = grads          # what the optimizer reads after finalize()
         self.bounds = list(bounds)
         self.active = force or comm.world_size > 1
         self.grad_scale = 1.0 / comm.world_size
         self._native = None
         self._pending = {}
-        if self.active and isinstance(comm, RcclComm):
+        self.kind = "local"
+        self.transport_note = ""
+        if not self.active:
+            return
+        transport = transport or default_transport()
+        if transport not in TRANSPORTS:
+            raise ValueError(f"transport {transport!r}: choose from {TRANSPORTS}")
+        # auto picks xgmi on the RCCL (GPU) data plane; an explicit xgmi also runs over a
+        # gloo control plane (two-ranks-on-one-GPU rehearsal, where RCCL refuses to run)
+        if grads.is_cuda and (transport == "xgmi" or
+                              (transport == "auto" and isinstance(comm, RcclComm))):
+            try:
+                x = XgmiTransport(comm, grads, self.bounds)
+            except Exception as e:           # mapping or self-check failed on some rank
+                if transport == "xgmi":
+                    raise
+                x = None
+                self.transport_note = f"xgmi unavailable ({e}); using rccl"
+            if x is not None:
+                self._native, self.kind, self.out_grads = x.native, "xgmi", x.result
+                self._xgmi = x
+                return
+        if isinstance(comm, RcclComm):
             C = _ext.require()
             flat = [b for se in self.bounds for b in se]
             self._native = C.GradReducer(comm.handle, grads, flat)
+            self.kind = "rccl"
+        else:
+            self.kind = "torch" if isinstance(comm, TorchComm) else "local"
+        if self.transport_note and comm.rank == 0:
+            print(f"warning: {self.transport_note}", file=sys.stderr, flush=True)
 
     @property
     def num_buckets(self) -> int:
@@ -91,7 +140,113 @@ class GradReducer:
             w.wait()
         self._pending.clear()
 
+    def check(self) -> None:
+        """Raise if the xgmi transport reported a peer timeout (no-op otherwise)."""
+        if self.kind == "xgmi":
+            self._xgmi.check()
+
+    def close(self) -> None:
+        if self.kind == "xgmi":
+            self._xgmi.close()
+
     @property
     def capturable(self) -> bool:
         """True when the whole reduce path can live inside a hipGraph."""
         return (not self.active) or self._native is not None
+
+
+class XgmiTransport:
+    """Builds and checks one rank's end of the direct xGMI all-reduce.
+
+    Collective over the control plane: every rank exports its uncached buffer
+    (hipIpcGetMemHandle), the handles go through the rendezvous store, every rank
+    maps its peers, and then every rank runs three all-reduces of integer-valued
+    patterns whose sums are exact and compares the result bit-for-bit.  The
+    outcome is agreed with a gloo MIN, so either every rank uses xgmi or none does.
+    """
+
+    _tags = 0
+
+    def __init__(self, comm: RcclComm, grads: torch.Tensor, bounds, timeout_s: float | None = None,
+                 mode: str | None = None):
+        C = _ext.require()
+        from .dist import control_barrier, default_store, distributed_is_initialized
+        ws, rank = comm.world_size, comm.rank
+        dev = grads.device.index or 0
+        mode = mode or os.environ.get("PDM_XGMI_MODE", "auto")
+        # bound on any wait for a peer inside the kernel (a late peer is an error, not a hang)
+        timeout_s = timeout_s or float(os.environ.get("PDM_XGMI_TIMEOUT", "60"))
+        flat = [b for se in bounds for b in se]
+        err = None
+        native = None
+        try:
+            native = C.XgmiReducer(rank, ws, dev, grads, flat, timeout_s, mode)
+            handle = native.ipc_handle()
+        except Exception as e:
+            err, handle = e, b""
+        handles = [handle]
+        if ws > 1:
+            XgmiTransport._tags += 1
+            key = f"pdm_amd/xgmi/{XgmiTransport._tags}"
+            store = default_store()
+            store.set(f"{key}/{rank}", handle)
+            handles = [handle if r == rank else store.get(f"{key}/{r}") for r in range(ws)]
+            if err is None and all(len(h) > 0 for h in handles):
+                try:
+                    native.open_peers([bytes(h) for h in handles])
+                except Exception as e:
+                    err = e
+            elif err is None:
+                err = RuntimeError("a peer could not export its xgmi buffer")
+        else:
+            if native is not None:
+                native.open_peers([bytes(handle)])
+        self.native = native
+
+        def agree(flag: bool) -> bool:
+            if ws > 1 and distributed_is_initialized():
+                t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+                return bool(t.item())
+            return flag
+
+        # every rank has mapped every peer before any rank launches a collective kernel
+        all_ok = agree(err is None) and agree(self._selfcheck(grads, bounds, ws, rank))
+        if ws > 1 and distributed_is_initialized():
+            control_barrier()
+        if not all_ok:
+            if native is not None:
+                native.close()
+            raise RuntimeError(f"xgmi transport check failed ({err or 'numerical self-check'})")
+        self.result = native.result()
+        self.describe = native.describe()
+
+    def _selfcheck(self, grads, bounds, ws, rank) -> bool:
+        result = self.native.result()
+        saved = grads.clone()
+        ok = True
+        n = grads.numel()
+        base = (torch.arange(n, device=grads.device, dtype=torch.int64) % 251 - 125).float()
+        for it in range(3):
+            grads.copy_(base * float((it + 1) * (rank + 1)))
+            self.native.all_ready()
+            self.native.finalize()
+            torch.cuda.synchronize(grads.device)
+            want = base * float((it + 1) * ws * (ws + 1) // 2)
+            for s, e in bounds:
+                ok = ok and torch.equal(result[s:e], want[s:e])
+        ok = ok and self.native.error() == 0
+        grads.copy_(saved)
+        torch.cuda.synchronize(grads.device)
+        return bool(ok)
+
+    def check(self) -> None:
+        e = self.native.error()
+        if e:
+            raise RuntimeError(f"xgmi all-reduce: a peer did not arrive within the timeout "
+                               f"(error bits {e:#x}); the gradients of this run are invalid")
+
+    def close(self) -> None:
+        if self.native is not None:
+            self.native.close()
+            self.native = None

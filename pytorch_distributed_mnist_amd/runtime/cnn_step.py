@@ -172,7 +172,7 @@ class CnnStep(GpuStepBase):
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
-        carry = self.reducer.active and getattr(self.reducer, "_native", None) is not None
+        carry = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
         for i in range(n):
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
 
@@ -199,6 +199,11 @@ class CnnStep(GpuStepBase):
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view())
+        xgmi = getattr(self.reducer, "kind", None) == "xgmi"
+        if xgmi:
+            # bucket 0 (fc, 4.7 MB) is complete: its xGMI all-reduce kernel is small enough
+            # to be co-resident with cnn_bwd, so it travels during the conv backward
+            self.reducer.bucket_ready(0)
         ipb = choose_ipb(B)
         C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
                   ipb, self.conv_slab)
@@ -208,6 +213,13 @@ class CnnStep(GpuStepBase):
             return
         C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
+        if xgmi:
+            # bucket 1 (conv, 75 KB, one-shot) queues behind bucket 0 on the xgmi stream;
+            # one optimizer launch over the reduced arena once both have landed
+            self.reducer.bucket_ready(1)
+            self.reducer.finalize()
+            self.launch_optimizer()
+            return
         if getattr(self.reducer, "_native", None) is None:
             # gloo data plane (rehearsal / CPU-staged): plain bucket order, one update
             self.reducer.bucket_ready(0)

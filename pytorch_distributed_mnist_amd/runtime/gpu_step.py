@@ -146,14 +146,15 @@ class GpuStepBase:
         segs = self._opt_segments if segments is None else segments
         o = self.opt
         g = o.param_groups[0]
+        grads = self.reducer.out_grads       # the xgmi transport's result arena, or in place
         if o.kind == "adam":
             b1, b2 = g["betas"]
-            self.C.optim_step(self.C.OPT_ADAM, self.arena.params, self.arena.grads, o.exp_avg,
+            self.C.optim_step(self.C.OPT_ADAM, self.arena.params, grads, o.exp_avg,
                               o.exp_avg_sq, o._lr_dev, o._step_dev, float(b1), float(b2),
                               float(g["eps"]), float(g["weight_decay"]), 0.0, 0.0, False,
                               float(self.reducer.grad_scale), segs)
         else:
-            self.C.optim_step(self.C.OPT_SGD, self.arena.params, self.arena.grads,
+            self.C.optim_step(self.C.OPT_SGD, self.arena.params, grads,
                               o.momentum_buffer, None, o._lr_dev, o._step_dev, 0.0, 0.0, 0.0,
                               float(g["weight_decay"]), float(g["momentum"]),
                               float(g["dampening"]), bool(g["nesterov"]),

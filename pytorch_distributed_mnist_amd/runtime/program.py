@@ -104,7 +104,7 @@ class TrainProgram:
 def build_local_program(arch: str, dtype: str, device, batch_size: int, train_split, test_split,
                         optimizer: str = "adam", lr: float = 1e-3, momentum: float = 0.9,
                         weight_decay: float = 1e-4, seed: int = 0, use_graphs: bool = True,
-                        comm=None, force_comm: bool = False):
+                        comm=None, force_comm: bool = False, transport: str | None = None):
     """Single-rank program without a process group (tests, bench at N=1, smoke)."""
     from types import SimpleNamespace
 
@@ -122,6 +122,7 @@ def build_local_program(arch: str, dtype: str, device, batch_size: int, train_sp
     opt = build_optimizer(optimizer, arena, SimpleNamespace(lr=lr, momentum=momentum,
                                                             weight_decay=weight_decay))
     comm = comm or LocalComm()
-    reducer = GradReducer(comm, arena.grads, spec.bucket_bounds(), force=force_comm)
+    reducer = GradReducer(comm, arena.grads, spec.bucket_bounds(), force=force_comm,
+                          transport=transport)
     return TrainProgram(arch, dtype, arena, opt, reducer, train_split, test_split, batch_size,
                         use_graphs=use_graphs)

@@ -45,3 +45,20 @@ def test_bench_two_rank_flow_rehearsal(gpu):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["global_batch"] == 2 * d["config"]["batch_per_rank"]
+
+
+def test_bench_two_rank_xgmi_rehearsal(gpu):
+    """The N>1 bench with the direct xGMI gradient transport: 2 ranks on one GPU (hipIpc
+    between the two processes, gloo control plane)."""
+    from conftest import free_port
+    env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_BENCH_BACKEND="gloo", PDM_COMM="xgmi")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--steps", "24", "--warmup", "4"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["grad_transport"] == "xgmi"

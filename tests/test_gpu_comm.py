@@ -28,7 +28,7 @@ def test_grad_reducer_forced_and_graph_captured(gpu):
     comm = _comm(gpu)
     grads = torch.randn(10000, device=gpu)
     ref = grads.clone()
-    red = GradReducer(comm, grads, [(0, 4096), (4096, 10000)], force=True)
+    red = GradReducer(comm, grads, [(0, 4096), (4096, 10000)], force=True, transport="rccl")
     assert red._native is not None and red.capturable
     red.bucket_ready(0)
     red.bucket_ready(1)
@@ -53,7 +53,7 @@ def test_grad_reducer_grouped_all_ready(gpu):
     comm = _comm(gpu)
     grads = torch.randn(10000, device=gpu)
     ref = grads.clone()
-    red = GradReducer(comm, grads, [(0, 4096), (4096, 10000)], force=True)
+    red = GradReducer(comm, grads, [(0, 4096), (4096, 10000)], force=True, transport="rccl")
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         grads.mul_(3.0)
@@ -80,7 +80,8 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu):
     for force in (False, True):
         comm = _comm(gpu) if force else None
         p = build_local_program("cnn", "bf16", "cuda", 256, train, test, optimizer="sgd", lr=0.05,
-                                momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=force)
+                                momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=force,
+                                transport="rccl")
         assert p.gpu.fuse_conv_reduce == (not force)
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(len(train), 1, 0, 0))

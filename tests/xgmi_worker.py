@@ -1,0 +1,148 @@
+"""Multi-rank worker for the xGMI transport tests (tests/test_gpu_xgmi.py).
+
+Launched with ``torch.distributed.run --nproc-per-node N`` and PDM_SHARE_DEVICE=1:
+every rank sits on device 0 over a gloo control plane — the only multi-rank GPU
+setup a one-GPU box allows (RCCL refuses two ranks on one device; hipIpc between
+processes on one device is allowed).  The peer mappings, flag protocol, one-shot
+and two-shot schedules and the graph capture are the same code that runs over
+xGMI between GPUs.  Writes one JSON file per rank into $PDM_XGMI_OUT.
+"""
+import json
+import os
+import sys
+from types import SimpleNamespace
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+FC, CONV = 1181120, 18880          # the CNN's bucket sizes (floats)
+_LOG = None
+
+
+def log(msg):
+    """Progress line into $PDM_XGMI_LOG_DIR/rank<r>.log (diagnosis of a stuck rank)."""
+    if _LOG is not None:
+        _LOG.write(msg + "\n")
+        _LOG.flush()
+
+
+def rank_order_sum(data, ws):
+    parts = [torch.zeros_like(data) for _ in range(ws)]
+    dist.all_gather(parts, data)
+    want = parts[0].clone()
+    for p in parts[1:]:
+        want += p
+    return want
+
+
+def check_collective(comm, dev, rank, ws, mode):
+    from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
+    os.environ["PDM_XGMI_MODE"] = mode
+    n = FC + CONV
+    grads = torch.zeros(n, device=dev)
+    red = GradReducer(comm, grads, [(0, FC), (FC, n)], transport="xgmi")
+    assert red.kind == "xgmi", red.kind
+    gen = torch.Generator().manual_seed(100 + rank)
+    ok = True
+    log(f"{mode}: reducer up {red._xgmi.describe}")
+    for _ in range(4):                                   # eager, bucket by bucket
+        data = torch.randn(n, generator=gen)
+        want = rank_order_sum(data, ws)
+        grads.copy_(data.to(dev))
+        red.bucket_ready(0)
+        red.bucket_ready(1)
+        red.finalize()
+        torch.cuda.synchronize()
+        ok = ok and torch.equal(red.out_grads.cpu(), want)
+        log(f"{mode}: eager ok={ok} err={red._xgmi.native.error()}")
+    # captured: 3 all-reduces per replay, data changed by a captured kernel in between
+    g = torch.cuda.CUDAGraph()
+    scale = torch.ones(1, device=dev)
+    with torch.cuda.graph(g):
+        for _ in range(3):
+            grads.mul_(scale)
+            red.all_ready()
+            red.finalize()
+    for it in range(3):
+        data = torch.randn(n, generator=gen)
+        want = rank_order_sum(data * (2.0 ** (it + 1)) ** 3, ws)
+        grads.copy_(data.to(dev))
+        scale.fill_(2.0 ** (it + 1))
+        g.replay()
+        torch.cuda.synchronize()
+        ok = ok and torch.equal(red.out_grads.cpu(), want)
+    log(f"{mode}: graph ok={ok}")
+    red.check()
+    desc = red._xgmi.describe
+    red.close()
+    return bool(ok), [d["mode"] for d in desc]
+
+
+def train_cnn(comm, dev, rank, ws, transport):
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.models.reference import MODULES
+    from pytorch_distributed_mnist_amd.models.specs import get_spec
+    from pytorch_distributed_mnist_amd.optim.flat import build_optimizer
+    from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
+    from pytorch_distributed_mnist_amd.runtime.arena import FlatArena
+    from pytorch_distributed_mnist_amd.runtime.program import TrainProgram
+    os.environ["PDM_XGMI_MODE"] = "auto"
+    torch.manual_seed(1234)
+    spec = get_spec("cnn")
+    arena = FlatArena(spec, dev)
+    arena.load_module(MODULES["cnn"]())
+    opt = build_optimizer("sgd", arena, SimpleNamespace(lr=0.05, momentum=0.9, weight_decay=1e-4))
+    red = GradReducer(comm, arena.grads, spec.bucket_bounds(), transport=transport)
+    train = synthetic_split(128 * ws * 9 + 40, True)
+    test = synthetic_split(256, False)
+    prog = TrainProgram("cnn", "bf16", arena, opt, red, train, test, 128, use_graphs=True)
+    opt.sync_hyperparams()
+    for epoch in range(2):
+        prog.set_train_indices(distributed_indices(len(train), ws, rank, epoch))
+        prog.train_epoch()
+        log(f"cnn {transport}: epoch {epoch} done")
+    torch.cuda.synchronize()
+    red.check()
+    kind = red.kind
+    out = arena.params.clone()
+    red.close()
+    return out, kind
+
+
+def main():
+    global _LOG
+    rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if os.environ.get("PDM_XGMI_LOG_DIR"):
+        os.makedirs(os.environ["PDM_XGMI_LOG_DIR"], exist_ok=True)
+        _LOG = open(os.path.join(os.environ["PDM_XGMI_LOG_DIR"], f"rank{rank}.log"), "w")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from pytorch_distributed_mnist_amd.parallel.comm import TorchComm
+    comm = TorchComm()
+    res = {"rank": rank}
+    for mode in ("one", "two", "auto"):
+        ok, modes = check_collective(comm, dev, rank, ws, mode)
+        res[mode] = ok
+        res[mode + "_modes"] = modes
+    p_x, kind_x = train_cnn(comm, dev, rank, ws, "xgmi")
+    p_g, kind_g = train_cnn(comm, dev, rank, ws, None)       # gloo data plane
+    res["cnn_kinds"] = [kind_x, kind_g]
+    res["cnn_max_diff"] = float((p_x - p_g).abs().max())
+    res["cnn_equal"] = bool(torch.equal(p_x, p_g))
+    # every rank holds the same replica
+    parts = [torch.zeros_like(p_x.cpu()) for _ in range(ws)]
+    dist.all_gather(parts, p_x.cpu())
+    res["replicas_equal"] = all(torch.equal(parts[0], q) for q in parts[1:])
+    with open(os.path.join(os.environ["PDM_XGMI_OUT"], f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
