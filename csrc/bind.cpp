@@ -6,6 +6,7 @@
 #include <torch/extension.h>
 
 #include "kernels.h"
+#include "xgmi.h"
 
 namespace py = pybind11;
 void register_comm(py::module& m);
@@ -34,6 +35,20 @@ void need_aligned(const void* p, int bytes, const char* name) {
 
 template <typename T>
 T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+// xgmi streamed-mode sync words (GradReducer(...).sync tensor, int32 [XG_LOC_WORDS])
+unsigned* opt_sync(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous() &&
+                  t->numel() >= XG_LOC_WORDS, "xgmi sync words must be an int32 device tensor of ",
+              XG_LOC_WORDS);
+  return reinterpret_cast<unsigned*>(t->data_ptr());
+}
+
+unsigned* xg_step(const c10::optional<at::Tensor>& t) {
+  unsigned* p = opt_sync(t);
+  return p ? p + XG_LOC_STEP : nullptr;
+}
 
 int64_t* opt_i64(const c10::optional<at::Tensor>& t) {
   if (!t.has_value() || !t->defined()) return nullptr;
@@ -76,7 +91,8 @@ void lin_train(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tensor 
 }
 
 void lin_reduce(at::Tensor slab, int64_t B, at::Tensor gW, at::Tensor gb, at::Tensor metrics,
-                c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1) {
+                c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1,
+                c10::optional<at::Tensor> xg) {
   c10::DeviceGuard g(slab.device());
   need(slab, at::kFloat, "slab");
   need(gW, at::kFloat, "gW");
@@ -88,7 +104,7 @@ void lin_reduce(at::Tensor slab, int64_t B, at::Tensor gW, at::Tensor gb, at::Te
   need_numel(metrics, 3, "metrics");
   launch_lin_reduce(slab.data_ptr<float>(), (int)nblk, gW.data_ptr<float>(), gb.data_ptr<float>(),
                     metrics.data_ptr<double>(), (int)B, opt_i64(c0), opt_i64(c1),
-                    cur_stream(slab));
+                    xg_step(xg), cur_stream(slab));
 }
 
 void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
@@ -137,7 +153,8 @@ void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tens
 void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::optional<at::Tensor> v,
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd,
                 double momentum, double dampening, bool nesterov, double grad_scale,
-                std::vector<py::tuple> segs) {
+                std::vector<py::tuple> segs, c10::optional<at::Tensor> xg, int64_t signal_ch,
+                std::vector<int64_t> waits, double timeout_s) {
   c10::DeviceGuard dg(p.device());
   need(p, at::kFloat, "params");
   need(g, at::kFloat, "grads");
@@ -186,6 +203,15 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
     s.nslab = 0;
     s.slab_col0 = 0;
     s.slab_stride = 0;
+    // waits: flat (channel, multiplier) per segment, channel -1 = no wait
+    s.wait_ch = -1;
+    s.wait_mult = 0;
+    if (!waits.empty()) {
+      TORCH_CHECK(waits.size() == 2 * segs.size(), "waits must hold (channel, mult) per segment");
+      s.wait_ch = (int32_t)waits[2 * i];
+      s.wait_mult = (uint32_t)waits[2 * i + 1];
+      TORCH_CHECK(s.wait_ch >= -1 && s.wait_ch < XG_MAX_CH, "bad wait channel");
+    }
     if (t.size() > 5 && !t[5].is_none()) {
       // (slab tensor, nslab, col0, stride): gradient = fixed-order sum over the slabs
       auto sl = t[5].cast<py::tuple>();
@@ -215,6 +241,12 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
       s.shadow_t = ptr<__bf16>(sh);
     }
   }
+  a.xg = opt_sync(xg);
+  a.xg_signal_ch = (int)signal_ch;
+  a.xg_timeout = (long long)(timeout_s * 1e8);
+  TORCH_CHECK(signal_ch >= -1 && signal_ch < XG_MAX_CH, "bad signal channel");
+  TORCH_CHECK(a.xg != nullptr || (signal_ch < 0 && waits.empty()),
+              "optimizer waits / signals need the xgmi sync words");
   launch_optim((int)kind, a, cur_stream(p));
 }
 
@@ -285,7 +317,8 @@ void fc1_fwd(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_
 void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Tensor wf2,
               at::Tensor bf2, at::Tensor ylab, bool train, c10::optional<at::Tensor> dh,
               c10::optional<at::Tensor> dht, int64_t ldt, c10::optional<at::Tensor> slab,
-              at::Tensor metrics, c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1) {
+              at::Tensor metrics, c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1,
+              c10::optional<at::Tensor> xg) {
   c10::DeviceGuard g(part.device());
   TORCH_CHECK(B >= 1, "B must be >= 1");
   need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
@@ -313,7 +346,7 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
   launch_cnn_head(part.data_ptr<float>(), (int)splitk, (int)B, bf1.data_ptr<float>(),
                   wf2.data_ptr<float>(), bf2.data_ptr<float>(), ylab.data_ptr<int32_t>(), train, pdh,
                   pdht, (int)ldt, pslab, metrics.data_ptr<double>(), opt_i64(c0), opt_i64(c1),
-                  cur_stream(part));
+                  train ? xg_step(xg) : nullptr, cur_stream(part));
 }
 
 void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Tensor wf1t,
@@ -343,7 +376,8 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
 }
 
 void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::Tensor pmask,
-             at::Tensor w2t, int64_t B, int64_t ipb, at::Tensor slab) {
+             at::Tensor w2t, int64_t B, int64_t ipb, at::Tensor slab,
+             c10::optional<at::Tensor> xg_sync) {
   c10::DeviceGuard g(xg.device());
   TORCH_CHECK(B >= 1 && ipb >= 1, "bad B/ipb");
   need_min(xg, at::kByte, B * 784, "xg");
@@ -356,7 +390,7 @@ void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::
   need_min(slab, at::kFloat, (int64_t)cnn_bwd_blocks((int)B, (int)ipb) * CNN_CONV_SLAB, "conv slab");
   launch_cnn_bwd(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
                  ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
-                 slab.data_ptr<float>(), cur_stream(xg));
+                 slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
 }
 
 void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, at::Tensor gw1,
@@ -394,10 +428,20 @@ PYBIND11_MODULE(_C, m) {
   m.attr("LIN_SLAB") = LIN_SLAB;
   m.attr("OPT_ADAM") = OPT_ADAM;
   m.attr("OPT_SGD") = OPT_SGD;
+  m.attr("XG_LOC_ERR") = XG_LOC_ERR;
+  m.attr("XG_LOC_STEP") = XG_LOC_STEP;
+  m.attr("XG_LOC_READY") = XG_LOC_READY;
+  m.attr("XG_LOC_DONE") = XG_LOC_DONE;
   m.def("lin_train", &lin_train);
-  m.def("lin_reduce", &lin_reduce);
+  m.def("lin_reduce", &lin_reduce, py::arg("slab"), py::arg("B"), py::arg("gW"), py::arg("gb"),
+        py::arg("metrics"), py::arg("c0"), py::arg("c1"), py::arg("xg") = py::none());
   m.def("lin_eval", &lin_eval);
-  m.def("optim_step", &optim_step);
+  m.def("optim_step", &optim_step, py::arg("kind"), py::arg("p"), py::arg("g"), py::arg("m"),
+        py::arg("v"), py::arg("lr"), py::arg("step"), py::arg("beta1"), py::arg("beta2"),
+        py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"),
+        py::arg("nesterov"), py::arg("grad_scale"), py::arg("segs"), py::arg("xg") = py::none(),
+        py::arg("signal_ch") = -1, py::arg("waits") = std::vector<int64_t>{},
+        py::arg("timeout_s") = 60.0);
   m.def("gather_epoch", &gather_epoch);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
   m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });
@@ -408,9 +452,14 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CNN_CONV_SLAB_DB1") = CNN_CONV_SLAB_DB1;
   m.def("cnn_fwd", &cnn_fwd);
   m.def("fc1_fwd", &fc1_fwd);
-  m.def("cnn_head", &cnn_head);
+  m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
+        py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
+        py::arg("dht"), py::arg("ldt"), py::arg("slab"), py::arg("metrics"), py::arg("c0"),
+        py::arg("c1"), py::arg("xg") = py::none());
   m.def("fc1_bwd", &fc1_bwd);
-  m.def("cnn_bwd", &cnn_bwd);
+  m.def("cnn_bwd", &cnn_bwd, py::arg("xg"), py::arg("w1"), py::arg("b1"), py::arg("dpool"),
+        py::arg("pmask"), py::arg("w2t"), py::arg("B"), py::arg("ipb"), py::arg("slab"),
+        py::arg("xg_sync") = py::none());
   m.def("conv_reduce", &conv_reduce);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk);
   m.def("read_stamps", &read_stamps);

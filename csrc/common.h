@@ -63,9 +63,11 @@ __device__ __forceinline__ float from_bf16(bf16 h) { return (float)h; }
   } while (0)
 #endif
 
-__device__ __forceinline__ void pdm_bump_counters(int64_t* c0, int64_t* c1) {
+__device__ __forceinline__ void pdm_bump_counters(int64_t* c0, int64_t* c1,
+                                                  unsigned* c2 = nullptr) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (c0) *c0 += 1;
     if (c1) *c1 += 1;
+    if (c2) *c2 += 1;   // xgmi streamed mode: step generation (csrc/xgmi.h)
   }
 }

@@ -15,7 +15,7 @@ void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_
                       int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W, const float* b,
                       float* slab, hipStream_t st);
 void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, double* metrics, int B,
-                       int64_t* c0, int64_t* c1, hipStream_t st);
+                       int64_t* c0, int64_t* c1, unsigned* c2, hipStream_t st);
 void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, const float* W,
                      const float* b, double* metrics, hipStream_t st);
 
@@ -40,6 +40,9 @@ struct OptSeg {
   const float* slab;
   int32_t nslab, slab_col0;
   int64_t slab_stride;
+  // optional (xgmi streamed mode): wait until DONE[wait_ch] >= wait_mult * STEP
+  int32_t wait_ch;
+  uint32_t wait_mult;
 };
 
 struct OptArgs {
@@ -55,6 +58,11 @@ struct OptArgs {
   float grad_scale;
   int nseg;
   OptSeg seg[OPT_MAX_SEG];
+  // xgmi streamed mode: local sync words; every workgroup first stores
+  // READY[signal_ch] = STEP (signal_ch < 0: none), then waits its segment's channel
+  unsigned* xg;
+  int xg_signal_ch;
+  long long xg_timeout;   // s_memrealtime ticks
 };
 
 void launch_optim(int kind, OptArgs& a, hipStream_t st);
@@ -90,14 +98,14 @@ void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, i
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
-                     hipStream_t st);
+                     unsigned* c2, hipStream_t st);
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
                     hipStream_t st);
 void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
                     const uint8_t* pmask, const __bf16* w2t, int B, int imgs_per_block, float* slab,
-                    hipStream_t st);
+                    unsigned* xg_sync, hipStream_t st);
 int cnn_bwd_blocks(int B, int imgs_per_block);
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st);

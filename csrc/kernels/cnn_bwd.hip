@@ -20,6 +20,7 @@
 //                and writes one fp32 slab per block (no atomics, deterministic).
 //   conv_reduce: fixed-order slab sum -> conv gradients (bucket 1 complete).
 #include "cnn_common.h"
+#include "xgmi.h"
 
 #include <cstdlib>
 
@@ -522,8 +523,11 @@ constexpr int DG_MTP = PDM_DG_MTP;       // tiles per dgrad pass on waves 4-7
 __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     const uint8_t* __restrict__ xg, const float* __restrict__ w1, const float* __restrict__ b1,
     const bf16* __restrict__ dpool, const uint8_t* __restrict__ pmask,
-    const bf16* __restrict__ w2t, int B, int ipb, float* __restrict__ slab) {
+    const bf16* __restrict__ w2t, int B, int ipb, float* __restrict__ slab, unsigned* xg_sync) {
   __shared__ __attribute__((aligned(16))) char smem[B_TOTAL];
+  // xgmi streamed mode: this kernel starting means fc1_bwd finished, i.e. the fc
+  // gradient bucket is complete -> hand it to the persistent collective (csrc/xgmi.h)
+  if (xg_sync != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xg_signal_ready(xg_sync, 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
@@ -758,9 +762,9 @@ int cnn_bwd_blocks(int B, int ipb) { return (B + ipb - 1) / ipb; }
 
 void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
                     const uint8_t* pmask, const __bf16* w2t, int B, int ipb, float* slab,
-                    hipStream_t st) {
+                    unsigned* xg_sync, hipStream_t st) {
   cnn_bwd_kernel<<<cnn_bwd_blocks(B, ipb), BWD_THREADS, 0, st>>>(xg, w1, b1, dpool, pmask, w2t, B,
-                                                                 ipb, slab);
+                                                                 ipb, slab, xg_sync);
 }
 
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,

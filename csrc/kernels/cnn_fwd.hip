@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
     const float* __restrict__ part, int S, int B, const float* __restrict__ bf1,
     const float* __restrict__ wf2, const float* __restrict__ bf2, const int32_t* __restrict__ ylab,
     bf16* __restrict__ dh, bf16* __restrict__ dht, int ldt, float* __restrict__ slab,
-    double* __restrict__ metrics, int64_t* c0, int64_t* c1) {
+    double* __restrict__ metrics, int64_t* c0, int64_t* c1, unsigned* c2) {
   static_assert(HEAD_ROWS == 4, "one wave per row, 4 waves");
   __shared__ float hs[HEAD_ROWS][HID];
   __shared__ float dhs[HEAD_ROWS][HID];
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
   if (tid < NCLS) out[NCLS * HID + tid] = sx;
   else if (tid >= 16 && tid < 16 + HID) out[NCLS * HID + NCLS + tid - 16] = sx;
   else if (tid == 254 || tid == 255) out[HEAD_SLAB - 2 + (tid - 254)] = sx;
-  pdm_bump_counters(c0, c1);
+  pdm_bump_counters(c0, c1, c2);
 }
 
 }  // namespace
@@ -411,15 +411,15 @@ void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, i
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
-                     hipStream_t st) {
+                     unsigned* c2, hipStream_t st) {
   const int groups = (train ? ldt : B + HEAD_ROWS - 1) / HEAD_ROWS;
   const int nblk = cnn_head_blocks(groups);
   if (train)
     cnn_head_kernel<true><<<nblk, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh, dht, ldt,
-                                                slab, metrics, c0, c1);
+                                                slab, metrics, c0, c1, c2);
   else
     cnn_head_kernel<false><<<nblk, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh, dht,
-                                                 ldt, slab, metrics, c0, c1);
+                                                 ldt, slab, metrics, c0, c1, c2);
 }
 
 int cnn_head_blocks(int groups) { return groups < CNN_HEAD_MAX_BLOCKS ? groups : CNN_HEAD_MAX_BLOCKS; }

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
 
 __global__ __launch_bounds__(256) void lin_reduce_kernel(
     const float* __restrict__ slab, int nblk, float* __restrict__ gW, float* __restrict__ gb,
-    double* __restrict__ metrics, int B, int64_t* c0, int64_t* c1) {
+    double* __restrict__ metrics, int B, int64_t* c0, int64_t* c1, unsigned* c2) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < N * K + N + 2) {
     float s = 0.f;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void lin_reduce_kernel(
     else if (e == N * K + N) { metrics[0] += sd; metrics[2] += (double)B; }
     else metrics[1] += sd;
   }
-  pdm_bump_counters(c0, c1);
+  pdm_bump_counters(c0, c1, c2);
 }
 
 __global__ __launch_bounds__(256) void lin_eval_kernel(
@@ -203,9 +203,9 @@ void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_
 }
 
 void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, double* metrics, int B,
-                       int64_t* c0, int64_t* c1, hipStream_t st) {
+                       int64_t* c0, int64_t* c1, unsigned* c2, hipStream_t st) {
   const int n = N * K + N + 2;
-  lin_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(slab, nblk, gW, gb, metrics, B, c0, c1);
+  lin_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(slab, nblk, gW, gb, metrics, B, c0, c1, c2);
 }
 
 void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, const float* W,

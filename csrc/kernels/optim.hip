@@ -15,6 +15,7 @@
 //     the transposed bf16 store stay coalesced.
 #include "common.h"
 #include "kernels.h"
+#include "xgmi.h"
 
 namespace {
 
@@ -82,6 +83,17 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     if ((int)blockIdx.x >= a.seg[i].first_block) si = i;
   const OptSeg& s = a.seg[si];
   const int lb = blockIdx.x - s.first_block;
+  if (a.xg != nullptr) {
+    // xgmi streamed mode: publish the last bucket (every workgroup stores the same value,
+    // so none depends on another being dispatched), then wait for this segment's bucket
+    __shared__ int s_go;
+    if (threadIdx.x == 0) {
+      if (a.xg_signal_ch >= 0) xg_signal_ready(a.xg, a.xg_signal_ch);
+      s_go = s.wait_ch < 0 || xg_wait_done(a.xg, s.wait_ch, s.wait_mult, a.xg_timeout);
+    }
+    __syncthreads();
+    if (!s_go) return;     // a peer never arrived: error bit set, the host raises
+  }
   const Hyper h = make_hyper<KIND>(a);
   float* __restrict__ P = a.p + s.offset;
   const float* __restrict__ G = a.g + s.offset;

@@ -87,13 +87,12 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
   return *s_ok != 0;
 }
 
-__global__ __launch_bounds__(XG_THREADS) __attribute__((amdgpu_waves_per_eu(10, 10)))
-void xgmi_allreduce_kernel(XgmiArgs a) {
-  __shared__ int s_ok;
-  const int w = blockIdx.x, W = gridDim.x, tid = threadIdx.x;
+// One channel's all-reduce for workgroup w of W (its slice of every chunk) at call
+// generation `gen`; false when a peer did not arrive before the deadline.
+__device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsigned gen,
+                                           long long deadline, int* s_ok) {
+  const int tid = threadIdx.x;
   const int N = a.nranks, r = a.rank;
-  const unsigned gen = a.gen[w] + 1;   // this workgroup's call count on this channel
-  const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
   const f32x4* src = reinterpret_cast<const f32x4*>(a.src);
   const long long n4 = a.n >> 2;
   const bool two = a.mode == XG_TWO_SHOT;
@@ -128,7 +127,7 @@ void xgmi_allreduce_kernel(XgmiArgs a) {
     }
   }
   signal_peers(a, 0, w, gen);
-  if (!wait_peers(a, 0, w, gen, deadline, &s_ok)) return;
+  if (!wait_peers(a, 0, w, gen, deadline, s_ok)) return false;
 
   // fixed rank-order sum of this rank's chunk (two-shot) / of the whole bucket (one-shot)
   {
@@ -161,13 +160,76 @@ void xgmi_allreduce_kernel(XgmiArgs a) {
   }
   if (two) {
     signal_peers(a, 1, w, gen);
-    if (!wait_peers(a, 1, w, gen, deadline, &s_ok)) return;
+    if (!wait_peers(a, 1, w, gen, deadline, s_ok)) return false;
   }
-  if (tid == 0) a.gen[w] = gen;
+  return true;
+}
+
+// One collective call (bucket_ready / all_ready API): grid = the channel's workgroups.
+__global__ __launch_bounds__(XG_THREADS) __attribute__((amdgpu_waves_per_eu(10, 10)))
+void xgmi_allreduce_kernel(XgmiArgs a) {
+  __shared__ int s_ok;
+  const int w = blockIdx.x;
+  const unsigned gen = a.gen[w] + 1;   // this workgroup's call count on this channel
+  const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
+  if (!xg_channel(a, w, gridDim.x, gen, deadline, &s_ok)) return;
+  if (threadIdx.x == 0) a.gen[w] = gen;
+}
+
+// Streamed mode (csrc/xgmi.h): `nsteps` steps x every channel in one launch, handed
+// off with the compute stream through the local READY / DONE words.
+__global__ __launch_bounds__(XG_THREADS) __attribute__((amdgpu_waves_per_eu(10, 10)))
+void xgmi_stream_kernel(XgmiStreamArgs s) {
+  __shared__ int s_ok;
+  const int w = blockIdx.x, tid = threadIdx.x;
+  unsigned* loc = s.loc;
+  unsigned step = loc[XG_LOC_LSTEP + w];
+  for (int k = 0; k < s.nsteps; ++k) {
+    ++step;
+    for (int c = 0; c < s.nch; ++c) {
+      const XgmiArgs& a = s.ch[c];
+      if (w >= a.nblk) continue;
+      const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
+      // wait for the compute stream to publish this step's bucket c
+      if (tid == 0) {
+        bool ok = true;
+        while ((int)(__hip_atomic_load(loc + XG_LOC_READY + c, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) - step) < 0) {
+          if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+            ok = false;
+            atomicOr(loc + XG_LOC_ERR, 8u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_ok = ok;
+      }
+      __syncthreads();
+      if (!s_ok) return;
+      const unsigned gen = a.gen[w] + 1;
+      if (!xg_channel(a, w, a.nblk, gen, deadline, &s_ok)) return;
+      // every byte this workgroup stored for the channel is drained (write-through), and
+      // every peer's bytes for its slice have arrived: count the workgroup done
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        a.gen[w] = gen;
+        __hip_atomic_fetch_add(loc + XG_LOC_DONE + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  if (tid == 0) loc[XG_LOC_LSTEP + w] = step;
 }
 
 }  // namespace
 
 void launch_xgmi_allreduce(const XgmiArgs& a, int nblk, hipStream_t st) {
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nblk), dim3(XG_THREADS), 0, st, a);
+}
+
+void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st) {
+  int grid = 1;
+  for (int c = 0; c < s.nch; ++c) grid = s.ch[c].nblk > grid ? s.ch[c].nblk : grid;
+  hipLaunchKernelGGL(xgmi_stream_kernel, dim3(grid), dim3(XG_THREADS), 0, st, s);
 }

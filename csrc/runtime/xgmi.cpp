@@ -121,7 +121,8 @@ class XgmiReducer {
       c.mode = two ? XG_TWO_SHOT : XG_ONE_SHOT;
       c.chunk = two ? (int64_t)round_up((size_t)((c.n + nranks - 1) / nranks), 64) : c.n;
       const int64_t c4 = c.chunk / 4;
-      c.nblk = (int)std::min<int64_t>(XG_MAX_WG, std::max<int64_t>(1, (c4 + XG_THREADS - 1) / XG_THREADS));
+      // the same workgroup split serves the per-call kernel and the persistent one
+      c.nblk = (int)std::min<int64_t>(XG_STREAM_WG, std::max<int64_t>(1, (c4 + XG_THREADS - 1) / XG_THREADS));
       c.stage_off = off;
       const size_t stage_floats = two ? (size_t)nranks * c.chunk : 2 * (size_t)nranks * c.n;
       TORCH_CHECK(stage_floats * 4 < (size_t)0x7fffffff, "stage area exceeds the 2 GB buffer window");
@@ -135,8 +136,8 @@ class XgmiReducer {
     heap_ = heap_rec_->ptr;
     // zeroed before this rank publishes its handle, so no peer can signal into stale flags
     XG_HIP_OK(hipMemset(heap_, 0, heap_bytes_));
-    XG_HIP_OK(hipMalloc(&local_, (XG_MAX_CH * XG_MAX_WG + 64) * sizeof(unsigned)));
-    XG_HIP_OK(hipMemset(local_, 0, (XG_MAX_CH * XG_MAX_WG + 64) * sizeof(unsigned)));
+    XG_HIP_OK(hipMalloc(&local_, XG_LOC_WORDS * sizeof(unsigned)));
+    XG_HIP_OK(hipMemset(local_, 0, XG_LOC_WORDS * sizeof(unsigned)));
     XG_HIP_OK(hipDeviceSynchronize());
     for (int r = 0; r < XG_MAX_RANKS; ++r) peers_[r] = nullptr;
     peers_[rank] = heap_;
@@ -210,6 +211,38 @@ class XgmiReducer {
     XG_HIP_OK(hipStreamWaitEvent(caller(), reduced_[i], 0));
   }
 
+  // streamed mode: one persistent collective launch covering the next `nsteps` steps
+  // (fork: ordered after the caller's stream); the step kernels hand buckets over
+  // through the sync words, end() joins the caller's stream back
+  void begin(int nsteps) {
+    TORCH_CHECK(open_ || nranks_ == 1, "open_peers() first");
+    TORCH_CHECK(nsteps >= 1, "nsteps must be >= 1");
+    hipStream_t cur = caller();
+    XG_HIP_OK(hipEventRecord(ready_[0], cur));
+    XG_HIP_OK(hipStreamWaitEvent(stream_, ready_[0], 0));
+    XgmiStreamArgs sa{};
+    for (size_t i = 0; i < ch_.size(); ++i) fill_args((int)i, sa.ch[i]);
+    sa.loc = static_cast<unsigned*>(local_);
+    sa.nch = (int)ch_.size();
+    sa.nsteps = nsteps;
+    launch_xgmi_stream(sa, stream_);
+    XG_HIP_OK(hipGetLastError());
+    pending_ = true;
+  }
+
+  void end() { finalize(); }
+
+  at::Tensor sync() const {
+    alive();
+    auto opts = at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device_);
+    return torch::from_blob(local_, {XG_LOC_WORDS}, [](void*) {}, opts);
+  }
+
+  int blocks(int i) const {
+    TORCH_CHECK(i >= 0 && i < (int)ch_.size(), "bad bucket index");
+    return ch_[i].nblk;
+  }
+
   void finalize() {
     if (!pending_) return;
     XG_HIP_OK(hipEventRecord(done_, stream_));
@@ -217,7 +250,9 @@ class XgmiReducer {
     pending_ = false;
   }
 
-  // error word: bit 0 / 1 = a workgroup gave up waiting for its peers in phase 0 / 1
+  // error word: bit 0 / 1 = a collective workgroup gave up waiting for its peers in
+  // phase 0 / 1; bit 2 = an optimizer workgroup gave up waiting for a bucket; bit 3 =
+  // the persistent collective gave up waiting for the compute stream
   int64_t error() {
     alive();
     XG_HIP_OK(hipStreamSynchronize(stream_));
@@ -267,11 +302,17 @@ class XgmiReducer {
     TORCH_CHECK(open_ || nranks_ == 1, "open_peers() first");
   }
   hipStream_t caller() const { return c10::hip::getCurrentHIPStream(device_).stream(); }
-  unsigned* err_ptr() const { return static_cast<unsigned*>(local_) + XG_MAX_CH * XG_MAX_WG; }
+  unsigned* err_ptr() const { return static_cast<unsigned*>(local_) + XG_LOC_ERR; }
 
   void launch(int i) {
-    const Channel& c = ch_[i];
     XgmiArgs a{};
+    fill_args(i, a);
+    launch_xgmi_allreduce(a, ch_[i].nblk, stream_);
+    XG_HIP_OK(hipGetLastError());
+  }
+
+  void fill_args(int i, XgmiArgs& a) const {
+    const Channel& c = ch_[i];
     for (int r = 0; r < XG_MAX_RANKS; ++r) {
       char* base = static_cast<char*>(r < nranks_ ? peers_[r] : nullptr);
       a.stage[r] = base ? reinterpret_cast<float*>(base + c.stage_off) : nullptr;
@@ -279,7 +320,7 @@ class XgmiReducer {
       a.flags[r] = base ? reinterpret_cast<unsigned*>(base) : nullptr;
     }
     a.src = grads_.data_ptr<float>() + c.start;
-    a.gen = static_cast<unsigned*>(local_) + i * XG_MAX_WG;
+    a.gen = static_cast<unsigned*>(local_) + XG_LOC_GEN + i * XG_MAX_WG;
     a.err = err_ptr();
     a.off = c.start;
     a.n = c.n;
@@ -289,8 +330,7 @@ class XgmiReducer {
     a.nranks = nranks_;
     a.ch = i;
     a.mode = c.mode;
-    launch_xgmi_allreduce(a, c.nblk, stream_);
-    XG_HIP_OK(hipGetLastError());
+    a.nblk = c.nblk;
   }
 
   int rank_, nranks_, device_;
@@ -322,6 +362,10 @@ void register_xgmi(py::module& m) {
       .def("all_ready", &XgmiReducer::all_ready)
       .def("wait_bucket", &XgmiReducer::wait_bucket)
       .def("finalize", &XgmiReducer::finalize)
+      .def("begin", &XgmiReducer::begin)
+      .def("end", &XgmiReducer::end)
+      .def("sync", &XgmiReducer::sync)
+      .def("blocks", &XgmiReducer::blocks)
       .def("error", &XgmiReducer::error)
       .def("describe", &XgmiReducer::describe)
       .def("close", &XgmiReducer::close)

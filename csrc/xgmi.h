@@ -42,6 +42,64 @@ struct XgmiArgs {
   long long chunk;                // two-shot chunk (floats, multiple of 64)
   long long timeout;              // spin limit, s_memrealtime ticks (100 MHz)
   int rank, nranks, ch, mode;
+  int nblk;                       // workgroups that carry this channel
 };
 
 void launch_xgmi_allreduce(const XgmiArgs& a, int nblk, hipStream_t st);
+
+// ---- streamed mode: one persistent collective launch per captured step sequence.
+// A hipGraph edge between two queues costs 5-10 us on MI355X (measured: fork after
+// fc1_bwd delayed cnn_bwd by 11 us, each join 6-10 us), more than the transfers
+// themselves, so the per-step hand-offs between the compute stream and the
+// collective are device-side words in the reducer's local buffer instead:
+//   the step's middle kernel (cnn_head / lin_reduce) bumps STEP;
+//   the kernel that starts after a bucket is complete (cnn_bwd for the fc bucket,
+//   the optimizer for the last bucket) stores READY[c] = STEP;
+//   the persistent kernel waits READY[c] >= its own step count, runs the channel,
+//   and every workgroup adds 1 to DONE[c];
+//   the optimizer's workgroups wait DONE[c] >= nblk_c * STEP before updating.
+// Local sync words (uint32) of the reducer's local buffer:
+constexpr int XG_LOC_GEN = 0;                        // [XG_MAX_CH][XG_MAX_WG] call counters
+constexpr int XG_LOC_ERR = XG_MAX_CH * XG_MAX_WG;    // error bits (2: optimizer wait timeout)
+constexpr int XG_LOC_STEP = XG_LOC_ERR + 1;          // step generation
+constexpr int XG_LOC_READY = XG_LOC_ERR + 8;         // [XG_MAX_CH]
+constexpr int XG_LOC_DONE = XG_LOC_ERR + 16;         // [XG_MAX_CH]
+constexpr int XG_LOC_LSTEP = XG_LOC_ERR + 64;        // [XG_MAX_WG] steps run by the streamed kernel
+constexpr int XG_LOC_WORDS = XG_LOC_LSTEP + XG_MAX_WG;
+constexpr int XG_STREAM_WG = 64;                     // workgroups of the persistent launch
+
+struct XgmiStreamArgs {
+  XgmiArgs ch[XG_MAX_CH];
+  unsigned* loc;                  // local sync words
+  int nch, nsteps;
+};
+
+void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st);
+
+// Device-side helpers shared by the compute kernels that signal / wait.
+#if defined(__HIPCC__)
+__device__ __forceinline__ void xg_signal_ready(unsigned* loc, int ch) {
+  const unsigned g = __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(loc + XG_LOC_READY + ch, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane polls DONE[ch] until it reaches mult * STEP (bounded), then an agent-scope
+// acquire; false (and error bit 2) on timeout.  Call from a single lane; the caller
+// barriers its workgroup afterwards.
+__device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mult,
+                                             long long timeout) {
+  const unsigned target =
+      mult * __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + timeout;
+  while ((int)(__hip_atomic_load(loc + XG_LOC_DONE + ch, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+      atomicOr(loc + XG_LOC_ERR, 4u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+#endif

@@ -81,6 +81,11 @@ class GradReducer:
             if x is not None:
                 self._native, self.kind, self.out_grads = x.native, "xgmi", x.result
                 self._xgmi = x
+                # streamed mode (default): one persistent collective launch per captured
+                # step sequence, hand-offs through device words (csrc/xgmi.h)
+                self.streamed = os.environ.get("PDM_XGMI_STREAM", "1") != "0"
+                self.sync = x.native.sync()
+                self.timeout_s = x.timeout_s
                 return
         if isinstance(comm, RcclComm):
             C = _ext.require()
@@ -92,9 +97,34 @@ class GradReducer:
         if self.transport_note and comm.rank == 0:
             print(f"warning: {self.transport_note}", file=sys.stderr, flush=True)
 
+    streamed = False          # xgmi streamed mode (set in __init__)
+
     @property
     def num_buckets(self) -> int:
         return len(self.bounds)
+
+    # -- xgmi streamed mode -------------------------------------------------------
+    def begin(self, nsteps: int) -> None:
+        """Launch the persistent collective for the next ``nsteps`` steps."""
+        self._native.begin(nsteps)
+
+    def end(self) -> None:
+        """Join the persistent collective back into the compute stream."""
+        self._native.end()
+
+    def bucket_of(self, offset: int) -> int:
+        for i, (s, e) in enumerate(self.bounds):
+            if s <= offset < e:
+                return i
+        raise ValueError(f"offset {offset} is in no bucket")
+
+    def waits_for(self, segments) -> list:
+        """Flat (channel, multiplier) per optimizer segment: wait for that segment's bucket."""
+        out = []
+        for sg in segments:
+            b = self.bucket_of(sg[0])
+            out += [b, self._native.blocks(b)]
+        return out
 
     def bucket_ready(self, i: int) -> None:
         if not self.active:
@@ -220,6 +250,7 @@ class XgmiTransport:
             raise RuntimeError(f"xgmi transport check failed ({err or 'numerical self-check'})")
         self.result = native.result()
         self.describe = native.describe()
+        self.timeout_s = timeout_s
 
     def _selfcheck(self, grads, bounds, ws, rank) -> bool:
         result = self.native.result()

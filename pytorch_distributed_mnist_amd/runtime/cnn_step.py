@@ -173,8 +173,13 @@ class CnnStep(GpuStepBase):
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
         carry = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
+        streamed = self.reducer.streamed
+        if streamed:
+            self.reducer.begin(n)        # one persistent xgmi collective for the n steps
         for i in range(n):
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
+        if streamed:
+            self.reducer.end()
 
     def _train_impl(self, B: int, carry_in: bool = False, carry_out: bool = False) -> None:
         """One training step (kernel chain in the module docstring).
@@ -184,6 +189,8 @@ class CnnStep(GpuStepBase):
         all-reduce overlaps cnn_fwd.  carry_out: leave this step's fc update to the next step.
         """
         C, P, G = self.C, self.P, self.G
+        red = self.reducer
+        xs = red.sync if red.streamed else None       # xgmi streamed-mode sync words
         ldt = -(-B // 32) * 32
         S = self.splitk_train
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
@@ -195,25 +202,35 @@ class CnnStep(GpuStepBase):
         C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
         C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab, True,
                    self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
-                   self.ctr[0:1], self.opt._step_dev)
+                   self.ctr[0:1], self.opt._step_dev, xs)
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view())
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
-        if xgmi:
+        early = xgmi and not red.streamed and os.environ.get("PDM_XGMI_EARLY", "1") != "0"
+        if early:
             # bucket 0 (fc, 4.7 MB) is complete: its xGMI all-reduce kernel is small enough
             # to be co-resident with cnn_bwd, so it travels during the conv backward
             self.reducer.bucket_ready(0)
         ipb = choose_ipb(B)
+        # streamed xgmi: cnn_bwd's first workgroup publishes the fc bucket to the
+        # persistent collective, which then reduces it beside cnn_bwd
         C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
-                  ipb, self.conv_slab)
+                  ipb, self.conv_slab, xs)
         if self.fuse_conv_reduce:
             # world_size 1: no all-reduce, the conv slab reduction runs inside the update
             self.launch_optimizer(self._fused_segments(C.cnn_bwd_nblk(B, ipb)))
             return
         C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
+        if xgmi and red.streamed:
+            # the optimizer publishes the conv bucket; its fc workgroups wait for bucket 0
+            # (long reduced by now), its conv workgroups for bucket 1
+            self.launch_optimizer(signal_ch=1)
+            return
         if xgmi:
+            if not early:
+                self.reducer.bucket_ready(0)
             # bucket 1 (conv, 75 KB, one-shot) queues behind bucket 0 on the xgmi stream;
             # one optimizer launch over the reduced arena once both have landed
             self.reducer.bucket_ready(1)

@@ -128,8 +128,13 @@ class GpuStepBase:
 
     def _train_seq(self, B: int, n: int) -> None:
         """n consecutive steps (captured together into one graph, or eager)."""
+        streamed = self.reducer.streamed
+        if streamed:
+            self.reducer.begin(n)        # one persistent collective launch for the n steps
         for _ in range(n):
             self._train_impl(B)
+        if streamed:
+            self.reducer.end()
 
     def _train_impl(self, B: int) -> None:
         raise NotImplementedError
@@ -139,11 +144,21 @@ class GpuStepBase:
         """[(offset, rows, cols, shadow|None, shadow_t|None)] covering the arena."""
         return [(0, 1, self.arena.spec.total, None, None)]
 
-    def launch_optimizer(self, segments=None) -> None:
-        """One fused optimizer launch over `segments` (default: every parameter)."""
+    def launch_optimizer(self, segments=None, signal_ch: int = -1) -> None:
+        """One fused optimizer launch over `segments` (default: every parameter).
+
+        xgmi streamed mode: every workgroup first publishes bucket `signal_ch` (>= 0) to
+        the persistent collective, then waits until its own segment's bucket is reduced.
+        """
         if self._opt_segments is None:
             self._opt_segments = self.optimizer_segments()
         segs = self._opt_segments if segments is None else segments
+        red = self.reducer
+        if red.streamed:
+            xg = dict(xg=red.sync, signal_ch=signal_ch, waits=red.waits_for(segs),
+                      timeout_s=red.timeout_s)
+        else:
+            xg = {}
         o = self.opt
         g = o.param_groups[0]
         grads = self.reducer.out_grads       # the xgmi transport's result arena, or in place
@@ -152,13 +167,13 @@ class GpuStepBase:
             self.C.optim_step(self.C.OPT_ADAM, self.arena.params, grads, o.exp_avg,
                               o.exp_avg_sq, o._lr_dev, o._step_dev, float(b1), float(b2),
                               float(g["eps"]), float(g["weight_decay"]), 0.0, 0.0, False,
-                              float(self.reducer.grad_scale), segs)
+                              float(self.reducer.grad_scale), segs, **xg)
         else:
             self.C.optim_step(self.C.OPT_SGD, self.arena.params, grads,
                               o.momentum_buffer, None, o._lr_dev, o._step_dev, 0.0, 0.0, 0.0,
                               float(g["weight_decay"]), float(g["momentum"]),
                               float(g["dampening"]), bool(g["nesterov"]),
-                              float(self.reducer.grad_scale), segs)
+                              float(self.reducer.grad_scale), segs, **xg)
 
     def invalidate_graphs(self) -> None:
         self.graphs.clear()
@@ -179,10 +194,15 @@ class LinearStep(GpuStepBase):
         C = self.C
         C.lin_train(self.train_images, self.train_labels, self.idx, self.ctr[0:1], self.bfull, B,
                     self.W, self.b, self.slab)
+        red = self.reducer
         C.lin_reduce(self.slab, B, self.gW, self.gb, self.metrics.train_view(), self.ctr[0:1],
-                     self.opt._step_dev)
-        self.reducer.bucket_ready(0)
-        self.reducer.finalize()
+                     self.opt._step_dev, red.sync if red.streamed else None)
+        if red.streamed:
+            # the optimizer publishes the bucket and waits for the persistent collective
+            self.launch_optimizer(signal_ch=0)
+            return
+        red.bucket_ready(0)
+        red.finalize()
         self.launch_optimizer()
 
     def evaluate(self) -> None:
