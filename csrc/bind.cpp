@@ -250,6 +250,25 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
   launch_optim((int)kind, a, cur_stream(p));
 }
 
+// xgmi streamed mode: publish bucket `signal_ch` (-1: none) and wait for the buckets in
+// `waits` = flat (channel, multiplier) pairs, on the current stream (one workgroup)
+void xgmi_wait(at::Tensor sync, int64_t signal_ch, std::vector<int64_t> waits, double timeout_s) {
+  c10::DeviceGuard g(sync.device());
+  unsigned* loc = opt_sync(sync);
+  TORCH_CHECK(waits.size() % 2 == 0 && waits.size() <= 8, "waits: up to 4 (channel, mult) pairs");
+  TORCH_CHECK(signal_ch >= -1 && signal_ch < XG_MAX_CH, "bad signal channel");
+  int ch[4];
+  unsigned mult[4];
+  const int n = (int)waits.size() / 2;
+  for (int i = 0; i < n; ++i) {
+    TORCH_CHECK(waits[2 * i] >= 0 && waits[2 * i] < XG_MAX_CH, "bad wait channel");
+    ch[i] = (int)waits[2 * i];
+    mult[i] = (unsigned)waits[2 * i + 1];
+  }
+  launch_xgmi_wait(loc, (int)signal_ch, n, ch, mult, (long long)(timeout_s * 1e8),
+                   cur_stream(sync));
+}
+
 // ------------------------------------------------------------------ CNN (bf16)
 void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* name) {
   need(t, dt, name);
@@ -443,6 +462,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("signal_ch") = -1, py::arg("waits") = std::vector<int64_t>{},
         py::arg("timeout_s") = 60.0);
   m.def("gather_epoch", &gather_epoch);
+  m.def("xgmi_wait", &xgmi_wait);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
   m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });
   m.attr("CNN_HEAD_SLAB") = CNN_HEAD_SLAB;

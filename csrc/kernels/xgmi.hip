@@ -26,7 +26,6 @@ namespace {
 
 constexpr int XG_SC0_SC1 = 17;              // aux bits of a system-scope write-through store
 constexpr int XG_RSRC_W3 = 0x00020000;      // raw buffer descriptor word 3 (gfx9 family)
-constexpr int XG_BATCH = 4;                 // loads kept in flight per lane before their use
 
 __device__ __forceinline__ unsigned flag_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -40,11 +39,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(float* base) {
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, XG_RSRC_W3);
 }
 
-__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, long long i4, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(i4 * 16), 0, XG_SC0_SC1);
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int i4, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, i4 * 16, 0, XG_SC0_SC1);
 }
 
-__device__ __forceinline__ long long clampll(long long v, long long lo, long long hi) {
+__device__ __forceinline__ int clampi(int v, int lo, int hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
@@ -77,7 +76,7 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // buffer_inv sc0 sc1
+    if (a.nranks > 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // buffer_inv sc0 sc1
     if (lane == 0) {
       *s_ok = ok;
       if (!ok) atomicOr(a.err, 1u << ph);
@@ -89,41 +88,44 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
 
 // One channel's all-reduce for workgroup w of W (its slice of every chunk) at call
 // generation `gen`; false when a peer did not arrive before the deadline.
+// BATCH: loads kept in flight per lane before their use (the persistent kernel uses 2 to
+// stay within the 32 registers per lane that cnn_bwd leaves free on a CU).  Indices are
+// 32-bit float4 counts (the host keeps every stage area below 2 GB).
+template <int BATCH>
 __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsigned gen,
                                            long long deadline, int* s_ok) {
   const int tid = threadIdx.x;
   const int N = a.nranks, r = a.rank;
   const f32x4* src = reinterpret_cast<const f32x4*>(a.src);
-  const long long n4 = a.n >> 2;
+  const int n4 = (int)(a.n >> 2);
   const bool two = a.mode == XG_TWO_SHOT;
   // two-shot: chunk d of the bucket belongs to rank d; one-shot: one "chunk" = the bucket
-  const long long c4 = two ? (a.chunk >> 2) : n4;
-  const long long per = (c4 + W - 1) / W;               // float4 per workgroup slice
-  const long long lo = (long long)w * per;
-  const long long par = two ? 0 : (gen & 1u);           // one-shot stage double buffer
-  const long long row4 = c4;                            // stage row length (float4)
+  const int c4 = two ? (int)(a.chunk >> 2) : n4;
+  const int per = (c4 + W - 1) / W;                     // float4 per workgroup slice
+  const int lo = w * per;
+  const int par = two ? 0 : (int)(gen & 1u);            // one-shot stage double buffer
+  const int row4 = c4;                                  // stage row length (float4)
 
   // phase 0: push slice w of chunk d (two-shot) / of the bucket (one-shot) into row r
   // of rank d's stage.  Workgroups start at different peers so all N-1 links carry
   // traffic at once; XG_BATCH loads are issued before their stores.
-  for (int i0 = 0; i0 < N - 1; i0 += XG_BATCH) {
-    int dd[XG_BATCH];
-    long long hid[XG_BATCH];
+  for (int i0 = 0; i0 < N - 1; i0 += BATCH) {
+    int dd[BATCH], hid[BATCH];
 #pragma unroll
-    for (int b = 0; b < XG_BATCH; ++b) {
+    for (int b = 0; b < BATCH; ++b) {
       const int i = i0 + b < N - 1 ? i0 + b : i0;
       dd[b] = (r + 1 + (i + w) % (N - 1)) % N;
-      const long long len = two ? clampll(n4 - (long long)dd[b] * c4, 0, c4) : n4;
+      const int len = two ? clampi(n4 - dd[b] * c4, 0, c4) : n4;
       hid[b] = i0 + b < N - 1 ? (lo + per < len ? lo + per : len) : 0;
     }
-    for (long long j = lo + tid; j < lo + per; j += XG_THREADS) {
-      f32x4 v[XG_BATCH];
+    for (int j = lo + tid; j < lo + per; j += XG_THREADS) {
+      f32x4 v[BATCH];
 #pragma unroll
-      for (int b = 0; b < XG_BATCH; ++b)
-        if (j < hid[b]) v[b] = src[(two ? (long long)dd[b] * c4 : 0) + j];
+      for (int b = 0; b < BATCH; ++b)
+        if (j < hid[b]) v[b] = src[(two ? dd[b] * c4 : 0) + j];
 #pragma unroll
-      for (int b = 0; b < XG_BATCH; ++b)
-        if (j < hid[b]) store_wt(rsrc(a.stage[dd[b]] + (par * N + r) * row4 * 4), j, v[b]);
+      for (int b = 0; b < BATCH; ++b)
+        if (j < hid[b]) store_wt(rsrc(a.stage[dd[b]] + (long long)(par * N + r) * row4 * 4), j, v[b]);
     }
   }
   signal_peers(a, 0, w, gen);
@@ -131,23 +133,23 @@ __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsi
 
   // fixed rank-order sum of this rank's chunk (two-shot) / of the whole bucket (one-shot)
   {
-    const long long base = two ? (long long)r * c4 : 0;
-    const long long len = two ? clampll(n4 - base, 0, c4) : n4;
-    const long long hi = lo + per < len ? lo + per : len;
+    const int base = two ? r * c4 : 0;
+    const int len = two ? clampi(n4 - base, 0, c4) : n4;
+    const int hi = lo + per < len ? lo + per : len;
     const f32x4* own = src + base;
-    const f32x4* stage = reinterpret_cast<const f32x4*>(a.stage[r]) + par * N * row4;
-    const long long res = a.off + base * 4;             // float offset in the result arena
-    for (long long j = lo + tid; j < hi; j += XG_THREADS) {
+    const f32x4* stage = reinterpret_cast<const f32x4*>(a.stage[r]) + (long long)par * N * row4;
+    const long long res = a.off + (long long)base * 4;  // float offset in the result arena
+    for (int j = lo + tid; j < hi; j += XG_THREADS) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int s0 = 0; s0 < N; s0 += XG_BATCH) {
-        f32x4 v[XG_BATCH];
+      for (int s0 = 0; s0 < N; s0 += BATCH) {
+        f32x4 v[BATCH];
 #pragma unroll
-        for (int b = 0; b < XG_BATCH; ++b) {
+        for (int b = 0; b < BATCH; ++b) {
           const int s = s0 + b;
-          if (s < N) v[b] = s == r ? own[j] : stage[(long long)s * row4 + j];
+          if (s < N) v[b] = s == r ? own[j] : stage[s * row4 + j];
         }
 #pragma unroll
-        for (int b = 0; b < XG_BATCH; ++b)
+        for (int b = 0; b < BATCH; ++b)
           if (s0 + b < N) acc = s0 + b == 0 ? v[b] : acc + v[b];
       }
       if (two) {
@@ -166,20 +168,18 @@ __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsi
 }
 
 // One collective call (bucket_ready / all_ready API): grid = the channel's workgroups.
-__global__ __launch_bounds__(XG_THREADS) __attribute__((amdgpu_waves_per_eu(10, 10)))
-void xgmi_allreduce_kernel(XgmiArgs a) {
+__global__ __launch_bounds__(XG_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
   __shared__ int s_ok;
   const int w = blockIdx.x;
   const unsigned gen = a.gen[w] + 1;   // this workgroup's call count on this channel
   const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
-  if (!xg_channel(a, w, gridDim.x, gen, deadline, &s_ok)) return;
+  if (!xg_channel<4>(a, w, gridDim.x, gen, deadline, &s_ok)) return;
   if (threadIdx.x == 0) a.gen[w] = gen;
 }
 
 // Streamed mode (csrc/xgmi.h): `nsteps` steps x every channel in one launch, handed
 // off with the compute stream through the local READY / DONE words.
-__global__ __launch_bounds__(XG_THREADS) __attribute__((amdgpu_waves_per_eu(10, 10)))
-void xgmi_stream_kernel(XgmiStreamArgs s) {
+__global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs s) {
   __shared__ int s_ok;
   const int w = blockIdx.x, tid = threadIdx.x;
   unsigned* loc = s.loc;
@@ -208,24 +208,55 @@ void xgmi_stream_kernel(XgmiStreamArgs s) {
       __syncthreads();
       if (!s_ok) return;
       const unsigned gen = a.gen[w] + 1;
-      if (!xg_channel(a, w, a.nblk, gen, deadline, &s_ok)) return;
+      if (!xg_channel<2>(a, w, a.nblk, gen, deadline, &s_ok)) return;
       // every byte this workgroup stored for the channel is drained (write-through), and
       // every peer's bytes for its slice have arrived: count the workgroup done
+      // (every result byte was stored write-through and is drained, and every peer's
+      // bytes arrived behind its flag + our system acquire: no release fence needed)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
         a.gen[w] = gen;
-        __hip_atomic_fetch_add(loc + XG_LOC_DONE + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(loc + XG_LOC_DONE + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
   if (tid == 0) loc[XG_LOC_LSTEP + w] = step;
 }
 
+// Streamed mode, compute side: one 64-thread workgroup publishes READY[signal_ch] and
+// waits until every listed channel is reduced for this step, so the optimizer after it
+// needs no waiting of its own.  A single spinning workgroup (instead of the optimizer's
+// whole grid) leaves the GPU to everything else, including other processes' kernels
+// when ranks share a device (the one-GPU rehearsal).
+__global__ __launch_bounds__(64) void xgmi_wait_kernel(unsigned* loc, int signal_ch, int nwait,
+                                                       int4 ch, uint4 mult, long long timeout) {
+  if (threadIdx.x != 0) return;
+  if (signal_ch >= 0) xg_signal_ready(loc, signal_ch);
+  const int c[4] = {ch.x, ch.y, ch.z, ch.w};
+  const unsigned m[4] = {mult.x, mult.y, mult.z, mult.w};
+  for (int i = 0; i < nwait; ++i)
+    if (!xg_wait_done(loc, c[i], m[i], timeout, /*acquire=*/false)) return;
+}
+
 }  // namespace
 
 void launch_xgmi_allreduce(const XgmiArgs& a, int nblk, hipStream_t st) {
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nblk), dim3(XG_THREADS), 0, st, a);
+}
+
+void launch_xgmi_wait(unsigned* loc, int signal_ch, int nwait, const int* ch, const unsigned* mult,
+                      long long timeout, hipStream_t st) {
+  int4 c = {0, 0, 0, 0};
+  uint4 m = {0, 0, 0, 0};
+  int* cp = &c.x;
+  unsigned* mp = &m.x;
+  for (int i = 0; i < nwait && i < 4; ++i) {
+    cp[i] = ch[i];
+    mp[i] = mult[i];
+  }
+  hipLaunchKernelGGL(xgmi_wait_kernel, dim3(1), dim3(64), 0, st, loc, signal_ch, nwait, c, m,
+                     timeout);
 }
 
 void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st) {

@@ -75,6 +75,9 @@ struct XgmiStreamArgs {
 };
 
 void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st);
+// compute side of streamed mode: READY[signal_ch] = STEP, then wait DONE[ch[i]] >= mult[i]*STEP
+void launch_xgmi_wait(unsigned* loc, int signal_ch, int nwait, const int* ch, const unsigned* mult,
+                      long long timeout, hipStream_t st);
 
 // Device-side helpers shared by the compute kernels that signal / wait.
 #if defined(__HIPCC__)
@@ -83,11 +86,13 @@ __device__ __forceinline__ void xg_signal_ready(unsigned* loc, int ch) {
   __hip_atomic_store(loc + XG_LOC_READY + ch, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One lane polls DONE[ch] until it reaches mult * STEP (bounded), then an agent-scope
-// acquire; false (and error bit 2) on timeout.  Call from a single lane; the caller
-// barriers its workgroup afterwards.
+// One lane polls DONE[ch] until it reaches mult * STEP (bounded), then (acquire) an
+// agent-scope acquire so this workgroup may read the reduced bytes; false (and error
+// bit 2) on timeout.  Call from a single lane; the caller barriers its workgroup
+// afterwards.  A kernel that only gates the NEXT kernel needs no acquire: that kernel
+// starts behind the boundary's own acquire.
 __device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mult,
-                                             long long timeout) {
+                                             long long timeout, bool acquire = true) {
   const unsigned target =
       mult * __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + timeout;
@@ -99,7 +104,7 @@ __device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mul
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 #endif

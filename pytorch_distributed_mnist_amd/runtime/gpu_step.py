@@ -16,6 +16,8 @@ CNN (bf16):  cnn_fwd -> fc1_fwd -> cnn_head -> fc1_bwd -> [all-reduce bucket 0]
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import _ext
@@ -147,18 +149,28 @@ class GpuStepBase:
     def launch_optimizer(self, segments=None, signal_ch: int = -1) -> None:
         """One fused optimizer launch over `segments` (default: every parameter).
 
-        xgmi streamed mode: every workgroup first publishes bucket `signal_ch` (>= 0) to
-        the persistent collective, then waits until its own segment's bucket is reduced.
+        xgmi streamed mode: bucket `signal_ch` (>= 0) is published to the persistent
+        collective and the update waits for the buckets its segments belong to — by a
+        one-workgroup wait kernel in front of it (default), or, with
+        PDM_XGMI_OPT_WAIT=1, by every optimizer workgroup for its own segment's bucket
+        (lets the fc update run while the conv bucket is still in flight, but parks the
+        optimizer's whole grid on the GPU meanwhile).
         """
         if self._opt_segments is None:
             self._opt_segments = self.optimizer_segments()
         segs = self._opt_segments if segments is None else segments
         red = self.reducer
+        xg = {}
         if red.streamed:
-            xg = dict(xg=red.sync, signal_ch=signal_ch, waits=red.waits_for(segs),
-                      timeout_s=red.timeout_s)
-        else:
-            xg = {}
+            waits = red.waits_for(segs)
+            if os.environ.get("PDM_XGMI_OPT_WAIT") == "1":
+                xg = dict(xg=red.sync, signal_ch=signal_ch, waits=waits, timeout_s=red.timeout_s)
+            else:
+                uniq = []
+                for i in range(0, len(waits), 2):
+                    if waits[i] not in uniq[0::2]:
+                        uniq += waits[i:i + 2]
+                self.C.xgmi_wait(red.sync, signal_ch, uniq, red.timeout_s)
         o = self.opt
         g = o.param_groups[0]
         grads = self.reducer.out_grads       # the xgmi transport's result arena, or in place

@@ -75,12 +75,14 @@ def test_cnn_step_through_xgmi_matches_local(gpu):
 
 
 def _run_workers(nproc, tmp_path):
-    env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_XGMI_OUT=str(tmp_path))
+    # a peer that never arrives turns into an error after 10 s instead of a 60 s stall
+    env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_XGMI_OUT=str(tmp_path),
+               PDM_XGMI_TIMEOUT=os.environ.get("PDM_XGMI_TIMEOUT", "10"))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
                         "--master-port", str(free_port()),
                         os.path.join(REPO, "tests", "xgmi_worker.py")],
-                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(nproc)]
 
