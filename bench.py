@@ -168,7 +168,27 @@ def main():
             use(red)
             run(16)
             calib[name] = timed(48) / 48 * 1e3
-            red.check()
+            try:
+                red.check()
+                ok = 1
+            except RuntimeError as e:
+                print(f"bench.py: {name} transport failed calibration: {e}", file=sys.stderr,
+                      flush=True)
+                ok = 0
+            if ws > 1:                         # every rank drops a transport any rank saw fail
+                t = torch.tensor([ok], dtype=torch.int32)
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+                ok = int(t.item())
+            if not ok:
+                if name == "rccl":
+                    raise RuntimeError("rccl transport failed calibration")
+                del calib[name]
+                torch.cuda.synchronize()
+                # replicas (and their momentum) may differ after a failed reduce
+                for t in (arena.params, *opt.state_buffers().values()):
+                    comm.broadcast_(t, 0)
+                if hasattr(prog.gpu, "refresh_shadows"):
+                    prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
         best = min(calib, key=calib.get)
         use(reducers[best])
     chosen = prog.reducer

@@ -29,6 +29,21 @@ def test_bench_json_contract(gpu):
     assert d["vs_baseline"] > 1.0
 
 
+def test_bench_transport_calibration(gpu):
+    """PDM_FORCE_COMM=1 at N=1 runs the multi-GPU step structure, so both gradient
+    transports (direct xGMI, RCCL) are built, calibrated on the real step, and the faster
+    one is timed."""
+    env = dict(os.environ, PDM_FORCE_COMM="1")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20",
+                        "--warmup", "3"], cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    cal = d["config"]["transport_calibration_ms_per_step"]
+    assert set(cal) == {"xgmi", "rccl"}, cal
+    assert d["config"]["grad_transport"] == min(cal, key=cal.get)
+
+
 def test_bench_two_rank_flow_rehearsal(gpu):
     """The N>1 driver path (torch.distributed.run, env rendezvous, barrier + max over ranks,
     rank-0 JSON) rehearsed with 2 ranks on one GPU over a gloo data plane."""
