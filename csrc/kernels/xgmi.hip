@@ -67,10 +67,13 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
     const bool mine = lane < a.nranks && lane != a.rank;
     const unsigned* f = a.flags[a.rank] + xg_flag_idx(a.ch, ph, mine ? lane : 0, w);
     bool ok = true;
-    for (;;) {
+    for (unsigned it = 1;; ++it) {
       const bool arrived = !mine || (int)(flag_load(f) - gen) >= 0;
       if (__all(arrived)) break;
-      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+      // give up at the deadline, or (checked every 64 polls) as soon as any wait of
+      // this rank already gave up: one missing peer costs one timeout, not one per call
+      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline ||
+          ((it & 63u) == 0 && __builtin_amdgcn_readfirstlane(flag_load(a.err)) != 0)) {
         ok = false;
         break;
       }
@@ -193,9 +196,12 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs 
       // wait for the compute stream to publish this step's bucket c
       if (tid == 0) {
         bool ok = true;
-        while ((int)(__hip_atomic_load(loc + XG_LOC_READY + c, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) - step) < 0) {
-          if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+        for (unsigned it = 1; (int)(__hip_atomic_load(loc + XG_LOC_READY + c, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) - step) < 0;
+             ++it) {
+          if ((long long)__builtin_amdgcn_s_memrealtime() > deadline ||
+              ((it & 63u) == 0 && __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) != 0)) {
             ok = false;
             atomicOr(loc + XG_LOC_ERR, 8u);
             break;

@@ -96,9 +96,13 @@ __device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mul
   const unsigned target =
       mult * __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + timeout;
-  while ((int)(__hip_atomic_load(loc + XG_LOC_DONE + ch, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-    if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+  for (unsigned it = 1; (int)(__hip_atomic_load(loc + XG_LOC_DONE + ch, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
+       ++it) {
+    // deadline, or (every 64 polls) an earlier give-up of this rank: fail fast
+    if ((long long)__builtin_amdgcn_s_memrealtime() > deadline ||
+        ((it & 63u) == 0 && __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) != 0)) {
       atomicOr(loc + XG_LOC_ERR, 4u);
       return false;
     }

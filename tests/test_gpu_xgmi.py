@@ -74,10 +74,11 @@ def test_cnn_step_through_xgmi_matches_local(gpu):
     assert torch.equal(out[0], out[1])
 
 
-def _run_workers(nproc, tmp_path):
+def _run_workers(nproc, tmp_path, **extra):
     # a peer that never arrives turns into an error after 10 s instead of a 60 s stall
     env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_XGMI_OUT=str(tmp_path),
                PDM_XGMI_TIMEOUT=os.environ.get("PDM_XGMI_TIMEOUT", "10"))
+    env.update(extra)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
                         "--master-port", str(free_port()),
@@ -107,3 +108,14 @@ def test_xgmi_four_ranks_one_gpu(gpu, tmp_path):
         # above, the two trainings only have to stay close (bf16 weights amplify the
         # last-bit differences over 20 SGD steps)
         assert d["cnn_max_diff"] < 5e-2, d
+
+
+def test_xgmi_absent_peer_fails_fast(gpu, tmp_path):
+    """A peer that never joins costs ONE timeout: after the first give-up every later
+    wait of that rank (12 collective launches + 6 finalizes here) sees the error word and
+    returns, and check() reports the invalid gradients instead of the run hanging."""
+    d = _run_workers(2, tmp_path, PDM_XGMI_TIMEOUT="2", PDM_XGMI_ABSENT="1")[0]
+    assert d["check_raised"], d
+    assert d["error"] != 0, d
+    # without fail-fast: >= 12 x 2 s; with it: the first timeout(s) only
+    assert d["elapsed_s"] < 8.0, d

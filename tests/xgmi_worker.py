@@ -114,6 +114,36 @@ def train_cnn(comm, dev, rank, ws, transport):
     return out, kind
 
 
+def absent_peer(comm, dev, rank, ws):
+    """Rank 0 runs eager all-reduces that no other rank joins: the first wait gives up
+    at the deadline, every later one fails fast on the error word."""
+    import time
+    from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
+    os.environ["PDM_XGMI_MODE"] = "auto"
+    n = FC + CONV
+    grads = torch.ones(n, device=dev)
+    red = GradReducer(comm, grads, [(0, FC), (FC, n)], transport="xgmi")
+    out = {}
+    if rank == 0:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(6):
+            red.bucket_ready(0)
+            red.bucket_ready(1)
+            red.finalize()
+        torch.cuda.synchronize()
+        out["elapsed_s"] = time.perf_counter() - t0
+        out["error"] = int(red._xgmi.native.error()) if hasattr(red, "_xgmi") else -1
+        try:
+            red.check()
+            out["check_raised"] = False
+        except RuntimeError:
+            out["check_raised"] = True
+    dist.barrier()                     # peers keep their mappings until rank 0 is done
+    red.close()
+    return out
+
+
 def main():
     global _LOG
     rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -126,6 +156,12 @@ def main():
     from pytorch_distributed_mnist_amd.parallel.comm import TorchComm
     comm = TorchComm()
     res = {"rank": rank}
+    if os.environ.get("PDM_XGMI_ABSENT") == "1":
+        res.update(absent_peer(comm, dev, rank, ws))
+        with open(os.path.join(os.environ["PDM_XGMI_OUT"], f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+        dist.destroy_process_group()
+        return
     for mode in ("one", "two", "auto"):
         ok, modes = check_collective(comm, dev, rank, ws, mode)
         res[mode] = ok
