@@ -192,6 +192,9 @@ def main():
         best = min(calib, key=calib.get)
         use(reducers[best])
     chosen = prog.reducer
+    # capture + upload the step graphs outside the timed window (a graph captured lazily
+    # on first use would put its capture inside a short timed run)
+    prog.gpu.prepare(B)
     run(a.warmup)
     elapsed = timed(a.steps)
     chosen.check()

@@ -431,6 +431,16 @@ void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, 
 
 int64_t cnn_bwd_nblk(int64_t B, int64_t ipb) { return cnn_bwd_blocks((int)B, (int)ipb); }
 
+// Upload an instantiated hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device
+// on the current stream, so its first replay inside a timed region costs the same as later ones.
+void graph_upload(int64_t exec, int64_t device) {
+  TORCH_CHECK(exec != 0, "graph_upload: graph is not instantiated");
+  c10::DeviceGuard g(c10::Device(c10::kCUDA, (c10::DeviceIndex)device));
+  hipStream_t s = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
+  hipError_t e = hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), s);
+  TORCH_CHECK(e == hipSuccess, "hipGraphUpload: ", hipGetErrorString(e));
+}
+
 at::Tensor read_stamps(const std::string& which) {
   at::Tensor t = at::zeros({256, 16}, at::TensorOptions().dtype(at::kLong));
   auto* p = reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>());
@@ -483,6 +493,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_reduce", &conv_reduce);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk);
   m.def("read_stamps", &read_stamps);
+  m.def("graph_upload", &graph_upload);
   register_comm(m);
   register_xgmi(m);
 }

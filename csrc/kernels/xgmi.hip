@@ -17,8 +17,9 @@
 //            any wave loads the handed-off bytes.
 // All hand-off memory is uncached (hipDeviceMallocUncached), so no L2 on either
 // side can hold a stale copy across calls.  Every spin is bounded: past
-// `timeout` ticks the workgroup records the phase in `err` and exits, so a dead
-// peer turns into a host-visible error instead of a hung GPU.
+// `timeout` ticks the workgroup records its cause in `err` (XG_ERR_*; the first
+// cause also in XG_LOC_FIRST) and exits, so a dead peer turns into a host-visible
+// error instead of a hung GPU.
 #include "common.h"
 #include "xgmi.h"
 
@@ -66,23 +67,27 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
     const int lane = threadIdx.x;
     const bool mine = lane < a.nranks && lane != a.rank;
     const unsigned* f = a.flags[a.rank] + xg_flag_idx(a.ch, ph, mine ? lane : 0, w);
-    bool ok = true;
-    for (unsigned it = 1;; ++it) {
+    unsigned cause = 0;
+    for (unsigned it = 0;; ++it) {
+      // the error word is read on the first poll and every 64th: a wait that starts after
+      // any wait of this rank gave up fails at once, so one missing peer costs one timeout
+      const unsigned e = xg_poll_err(it) ? __builtin_amdgcn_readfirstlane(flag_load(a.err)) : 0u;
       const bool arrived = !mine || (int)(flag_load(f) - gen) >= 0;
+      if (e != 0) {
+        cause = XG_ERR_FAILFAST;
+        break;
+      }
       if (__all(arrived)) break;
-      // give up at the deadline, or (checked every 64 polls) as soon as any wait of
-      // this rank already gave up: one missing peer costs one timeout, not one per call
-      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline ||
-          ((it & 63u) == 0 && __builtin_amdgcn_readfirstlane(flag_load(a.err)) != 0)) {
-        ok = false;
+      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+        cause = ph == 0 ? XG_ERR_PEER0 : XG_ERR_PEER1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
     if (a.nranks > 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // buffer_inv sc0 sc1
     if (lane == 0) {
-      *s_ok = ok;
-      if (!ok) atomicOr(a.err, 1u << ph);
+      *s_ok = cause == 0;
+      if (cause != 0) xg_record_error(a.err, cause);
     }
   }
   __syncthreads();
@@ -196,14 +201,20 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs 
       // wait for the compute stream to publish this step's bucket c
       if (tid == 0) {
         bool ok = true;
-        for (unsigned it = 1; (int)(__hip_atomic_load(loc + XG_LOC_READY + c, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT) - step) < 0;
-             ++it) {
-          if ((long long)__builtin_amdgcn_s_memrealtime() > deadline ||
-              ((it & 63u) == 0 && __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+        for (unsigned it = 0;; ++it) {
+          const unsigned e = xg_poll_err(it) ? __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT) : 0u;
+          const unsigned ready = __hip_atomic_load(loc + XG_LOC_READY + c, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+          if (e != 0) {                    // this rank already gave up somewhere: fail fast
             ok = false;
-            atomicOr(loc + XG_LOC_ERR, 8u);
+            xg_record_error(loc + XG_LOC_ERR, XG_ERR_FAILFAST);
+            break;
+          }
+          if ((int)(ready - step) >= 0) break;
+          if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+            ok = false;
+            xg_record_error(loc + XG_LOC_ERR, XG_ERR_READY);
             break;
           }
           __builtin_amdgcn_s_sleep(1);

@@ -250,16 +250,13 @@ class XgmiReducer {
     pending_ = false;
   }
 
-  // error word: bit 0 / 1 = a collective workgroup gave up waiting for its peers in
-  // phase 0 / 1; bit 2 = an optimizer workgroup gave up waiting for a bucket; bit 3 =
-  // the persistent collective gave up waiting for the compute stream
-  int64_t error() {
-    alive();
-    XG_HIP_OK(hipStreamSynchronize(stream_));
-    unsigned e = 0;
-    XG_HIP_OK(hipMemcpy(&e, err_ptr(), sizeof(e), hipMemcpyDeviceToHost));
-    return e;
-  }
+  // error word (XG_ERR_* in xgmi.h): every cause any wait gave up for, including
+  // XG_ERR_FAILFAST for waits that only saw an earlier error
+  int64_t error() { return read_err_words().first; }
+
+  // the cause bit of the first wait that gave up at its deadline (0: none)
+  int64_t first_error() { return read_err_words().second; }
+
 
   py::list describe() const {
     py::list out;
@@ -303,6 +300,14 @@ class XgmiReducer {
   }
   hipStream_t caller() const { return c10::hip::getCurrentHIPStream(device_).stream(); }
   unsigned* err_ptr() const { return static_cast<unsigned*>(local_) + XG_LOC_ERR; }
+
+  std::pair<unsigned, unsigned> read_err_words() {
+    alive();
+    XG_HIP_OK(hipStreamSynchronize(stream_));
+    unsigned w[XG_LOC_FIRST - XG_LOC_ERR + 1] = {};
+    XG_HIP_OK(hipMemcpy(w, err_ptr(), sizeof(w), hipMemcpyDeviceToHost));
+    return {w[0], w[XG_LOC_FIRST - XG_LOC_ERR]};
+  }
 
   void launch(int i) {
     XgmiArgs a{};
@@ -367,6 +372,7 @@ void register_xgmi(py::module& m) {
       .def("sync", &XgmiReducer::sync)
       .def("blocks", &XgmiReducer::blocks)
       .def("error", &XgmiReducer::error)
+      .def("first_error", &XgmiReducer::first_error)
       .def("describe", &XgmiReducer::describe)
       .def("close", &XgmiReducer::close)
       .def_property_readonly("num_buckets", &XgmiReducer::num_buckets);

@@ -36,7 +36,7 @@ struct XgmiArgs {
   unsigned* flags[XG_MAX_RANKS];  // flag block on every rank
   const float* src;               // this rank's gradient bucket (bucket start)
   unsigned* gen;                  // this rank's per-workgroup call counters of the channel
-  unsigned* err;                  // this rank's error word (bit 0: phase-0 timeout, bit 1: phase 1)
+  unsigned* err;                  // this rank's error word (XG_ERR_* bits; XG_LOC_FIRST follows)
   long long off;                  // bucket start in the arena (floats)
   long long n;                    // bucket length (floats, multiple of 64)
   long long chunk;                // two-shot chunk (floats, multiple of 64)
@@ -60,8 +60,9 @@ void launch_xgmi_allreduce(const XgmiArgs& a, int nblk, hipStream_t st);
 //   the optimizer's workgroups wait DONE[c] >= nblk_c * STEP before updating.
 // Local sync words (uint32) of the reducer's local buffer:
 constexpr int XG_LOC_GEN = 0;                        // [XG_MAX_CH][XG_MAX_WG] call counters
-constexpr int XG_LOC_ERR = XG_MAX_CH * XG_MAX_WG;    // error bits (2: optimizer wait timeout)
+constexpr int XG_LOC_ERR = XG_MAX_CH * XG_MAX_WG;    // error bits (XG_ERR_*)
 constexpr int XG_LOC_STEP = XG_LOC_ERR + 1;          // step generation
+constexpr int XG_LOC_FIRST = XG_LOC_ERR + 2;         // the first error's cause bit (set once)
 constexpr int XG_LOC_READY = XG_LOC_ERR + 8;         // [XG_MAX_CH]
 constexpr int XG_LOC_DONE = XG_LOC_ERR + 16;         // [XG_MAX_CH]
 constexpr int XG_LOC_LSTEP = XG_LOC_ERR + 64;        // [XG_MAX_WG] steps run by the streamed kernel
@@ -79,31 +80,57 @@ void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st);
 void launch_xgmi_wait(unsigned* loc, int signal_ch, int nwait, const int* ch, const unsigned* mult,
                       long long timeout, hipStream_t st);
 
+// Error bits of the rank's error word (XG_LOC_ERR).  A wait that runs past its deadline
+// records its own cause; a wait that gives up because the word was already set records
+// XG_ERR_FAILFAST only, and the first cause is kept separately in XG_LOC_FIRST, so the
+// host can tell the root cause from its consequences.
+constexpr unsigned XG_ERR_PEER0 = 1u;      // a collective workgroup's peers missed phase 0
+constexpr unsigned XG_ERR_PEER1 = 2u;      // ... phase 1 (two-shot all-gather)
+constexpr unsigned XG_ERR_OPTWAIT = 4u;    // the optimizer side waited for a bucket in vain
+constexpr unsigned XG_ERR_READY = 8u;      // the persistent collective waited for the compute stream
+constexpr unsigned XG_ERR_FAILFAST = 16u;  // a wait gave up because an earlier one had
+
 // Device-side helpers shared by the compute kernels that signal / wait.
 #if defined(__HIPCC__)
+// `err` points at XG_LOC_ERR of the rank's local words.
+__device__ __forceinline__ void xg_record_error(unsigned* err, unsigned bit) {
+  atomicOr(err, bit);
+  if (bit != XG_ERR_FAILFAST) atomicCAS(err + (XG_LOC_FIRST - XG_LOC_ERR), 0u, bit);
+}
+
+// Poll schedule shared by every bounded wait: the error word is read on the first poll
+// and every 64th after it, so a wait that starts after this rank's error word was set
+// gives up at once (deterministically), and one missing peer costs one timeout.
+__device__ __forceinline__ bool xg_poll_err(unsigned it) { return (it & 63u) == 0; }
+
 __device__ __forceinline__ void xg_signal_ready(unsigned* loc, int ch) {
   const unsigned g = __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(loc + XG_LOC_READY + ch, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One lane polls DONE[ch] until it reaches mult * STEP (bounded), then (acquire) an
-// agent-scope acquire so this workgroup may read the reduced bytes; false (and error
-// bit 2) on timeout.  Call from a single lane; the caller barriers its workgroup
-// afterwards.  A kernel that only gates the NEXT kernel needs no acquire: that kernel
+// agent-scope acquire so this workgroup may read the reduced bytes; false (and
+// XG_ERR_OPTWAIT, or XG_ERR_FAILFAST after an earlier error) when it gives up.
+// Call from a single lane; the caller barriers its workgroup afterwards.  A kernel that only gates the NEXT kernel needs no acquire: that kernel
 // starts behind the boundary's own acquire.
 __device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mult,
                                              long long timeout, bool acquire = true) {
   const unsigned target =
       mult * __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + timeout;
-  for (unsigned it = 1; (int)(__hip_atomic_load(loc + XG_LOC_DONE + ch, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
-       ++it) {
-    // deadline, or (every 64 polls) an earlier give-up of this rank: fail fast
-    if ((long long)__builtin_amdgcn_s_memrealtime() > deadline ||
-        ((it & 63u) == 0 && __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-      atomicOr(loc + XG_LOC_ERR, 4u);
+  for (unsigned it = 0;; ++it) {
+    // both loads are issued before either is consumed: the error check adds no latency
+    const unsigned e = xg_poll_err(it) ? __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const unsigned done = __hip_atomic_load(loc + XG_LOC_DONE + ch, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0) {                        // an earlier wait of this rank gave up: fail fast
+      xg_record_error(loc + XG_LOC_ERR, XG_ERR_FAILFAST);
+      return false;
+    }
+    if ((int)(done - target) >= 0) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+      xg_record_error(loc + XG_LOC_ERR, XG_ERR_OPTWAIT);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);

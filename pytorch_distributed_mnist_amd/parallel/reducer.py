@@ -271,11 +271,26 @@ class XgmiTransport:
         torch.cuda.synchronize(grads.device)
         return bool(ok)
 
+    # cause bits of the device error word (csrc/xgmi.h XG_ERR_*)
+    CAUSES = {1: "a peer did not arrive for the reduce-scatter / push phase",
+              2: "a peer did not arrive for the all-gather phase",
+              4: "the optimizer waited in vain for a reduced bucket",
+              8: "the persistent collective waited in vain for this rank's backward to "
+                 "publish a bucket",
+              16: "waits that gave up after an earlier error (fail-fast)"}
+
+    @classmethod
+    def describe_error(cls, bits: int, first: int) -> str:
+        what = [cls.CAUSES[b] for b in sorted(cls.CAUSES) if bits & b]
+        root = cls.CAUSES.get(first, f"unknown cause {first:#x}") if first else "none recorded"
+        return f"first cause: {root}; all causes (bits {bits:#x}): " + "; ".join(what)
+
     def check(self) -> None:
         e = self.native.error()
         if e:
-            raise RuntimeError(f"xgmi all-reduce: a peer did not arrive within the timeout "
-                               f"(error bits {e:#x}); the gradients of this run are invalid")
+            first = self.native.first_error()
+            raise RuntimeError(f"xgmi all-reduce timed out ({self.describe_error(e, first)}); "
+                               f"the gradients of this run are invalid")
 
     def close(self) -> None:
         if self.native is not None:

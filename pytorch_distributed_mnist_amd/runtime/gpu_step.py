@@ -94,8 +94,9 @@ class GpuStepBase:
     # list, graph-replay-floor) — more than a whole small step's GPU time — so
     # steps are captured GRAPH_STEPS at a time (identical steps: the batch comes
     # from the device counter) and a run of n steps replays n // GRAPH_STEPS
-    # multi-step graphs plus single-step graphs for the remainder.
+    # multi-step graphs plus one graph per set bit of the remainder (4, 2, 1 steps).
     GRAPH_STEPS = 8
+    GRAPH_SIZES = (8, 4, 2, 1)
 
     def _graph(self, B: int, nsteps: int):
         key = (B, nsteps)
@@ -107,6 +108,21 @@ class GpuStepBase:
             self.graphs[key] = g
         return g
 
+    def prepare(self, B: int) -> None:
+        """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES), so no
+        capture or first-launch upload lands inside a timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
+        when replayed."""
+        if not self.use_graphs:
+            return
+        for n in self.GRAPH_SIZES:
+            g = self._graph(B, n)
+            try:
+                exe = g.raw_cuda_graph_exec()
+            except (AttributeError, RuntimeError):
+                continue
+            self.C.graph_upload(int(exe), self.device.index or 0)
+        torch.cuda.synchronize(self.device)
+
     def train_steps(self, B: int, n: int) -> None:
         """Enqueue n consecutive training steps of batch size B."""
         if n <= 0:
@@ -117,10 +133,10 @@ class GpuStepBase:
                 gk = self._graph(B, k)
                 for _ in range(n // k):
                     gk.replay()
-            if n % k:
-                g1 = self._graph(B, 1)
-                for _ in range(n % k):
-                    g1.replay()
+            r = n % k
+            for size in self.GRAPH_SIZES[1:]:
+                if r & size:
+                    self._graph(B, size).replay()
         else:
             self._train_seq(B, n)
         self.opt.step_count += n

@@ -119,3 +119,19 @@ def test_xgmi_absent_peer_fails_fast(gpu, tmp_path):
     assert d["error"] != 0, d
     # without fail-fast: >= 12 x 2 s; with it: the first timeout(s) only
     assert d["elapsed_s"] < 8.0, d
+
+
+def test_xgmi_absent_peer_fails_fast_streamed(gpu, tmp_path):
+    """The same through the default streamed mode: 19 graph-replayed CNN steps (four
+    persistent collective launches: 8 + 8 + 2 + 1 steps) on rank 0 whose peer never
+    runs a step.  The collective's first phase-0 wait times out (the recorded first
+    cause); every optimizer-side wait and every later READY / peer wait fails fast, so the
+    run costs about one timeout instead of one per step, and check() names the cause."""
+    d = _run_workers(2, tmp_path, PDM_XGMI_TIMEOUT="2", PDM_XGMI_ABSENT="streamed")[0]
+    assert d["streamed"], d
+    assert d["check_raised"], d
+    assert d["first_error"] == 1, d                  # XG_ERR_PEER0: the root cause
+    assert d["error"] & 16, d                        # later waits failed fast
+    assert "first cause: a peer did not arrive" in d["message"], d
+    # without fail-fast: one 2 s timeout per step (>= 38 s); with it: about one
+    assert d["elapsed_s"] < 8.0, d

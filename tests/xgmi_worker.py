@@ -144,6 +144,53 @@ def absent_peer(comm, dev, rank, ws):
     return out
 
 
+def absent_peer_streamed(comm, dev, rank, ws):
+    """Streamed mode (the default): rank 0 trains CNN steps whose persistent collective
+    never sees its peer.  The collective's first phase-0 wait gives up at the deadline;
+    the optimizer-side waits of every later step and the persistent kernel's READY
+    waits fail fast on the error word, so the whole run costs about one timeout."""
+    import time
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.models.reference import MODULES
+    from pytorch_distributed_mnist_amd.models.specs import get_spec
+    from pytorch_distributed_mnist_amd.optim.flat import build_optimizer
+    from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
+    from pytorch_distributed_mnist_amd.runtime.arena import FlatArena
+    from pytorch_distributed_mnist_amd.runtime.program import TrainProgram
+    os.environ["PDM_XGMI_MODE"] = "auto"
+    spec = get_spec("cnn")
+    arena = FlatArena(spec, dev)
+    arena.load_module(MODULES["cnn"]())
+    red = GradReducer(comm, arena.grads, spec.bucket_bounds(), transport="xgmi")
+    out = {"streamed": bool(red.streamed)}
+    if rank == 0:
+        opt = build_optimizer("sgd", arena, SimpleNamespace(lr=0.05, momentum=0.9,
+                                                            weight_decay=1e-4))
+        train = synthetic_split(64 * 40, True)
+        prog = TrainProgram("cnn", "bf16", arena, opt, red, train, synthetic_split(64, False),
+                            64, use_graphs=True)
+        opt.sync_hyperparams()
+        prog.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        prog.gpu.prepare(64)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        prog.gpu.train_steps(64, 2 * prog.gpu.GRAPH_STEPS + 3)     # graphs of 8, 8, 2, 1 steps
+        torch.cuda.synchronize()
+        out["elapsed_s"] = time.perf_counter() - t0
+        out["error"] = int(red._xgmi.native.error())
+        out["first_error"] = int(red._xgmi.native.first_error())
+        try:
+            red.check()
+            out["check_raised"] = False
+        except RuntimeError as e:
+            out["check_raised"] = True
+            out["message"] = str(e)
+    dist.barrier()                     # peers keep their mappings until rank 0 is done
+    red.close()
+    return out
+
+
 def main():
     global _LOG
     rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -156,8 +203,10 @@ def main():
     from pytorch_distributed_mnist_amd.parallel.comm import TorchComm
     comm = TorchComm()
     res = {"rank": rank}
-    if os.environ.get("PDM_XGMI_ABSENT") == "1":
-        res.update(absent_peer(comm, dev, rank, ws))
+    absent = os.environ.get("PDM_XGMI_ABSENT")
+    if absent in ("1", "streamed"):
+        res.update(absent_peer(comm, dev, rank, ws) if absent == "1" else
+                   absent_peer_streamed(comm, dev, rank, ws))
         with open(os.path.join(os.environ["PDM_XGMI_OUT"], f"rank{rank}.json"), "w") as f:
             json.dump(res, f)
         dist.destroy_process_group()
