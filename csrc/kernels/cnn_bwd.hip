@@ -23,10 +23,22 @@
 #include "xgmi.h"
 
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 namespace {
 
 using namespace cnn;
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1, fully expanded
+template <class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // ------------------------------------------------------------------ fc1_bwd
 constexpr int DW_TILES = FEAT / 64;  // 144
@@ -67,7 +79,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const int srow = tid >> 3, sch = tid & 7;
     uint4 pv[DWC / 32];
     bf16x8 a[2][DWC / 32];
-    auto load_chunk = [&](int c0) {
+    auto load_chunk = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < DWC / 32; ++j) {
         const int row = c0 + srow + 32 * j;
@@ -217,61 +229,74 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 }
 
 // ------------------------------------------------------------------ cnn_bwd
+// LDS carve (one static array, 162,688 B -> 1 workgroup / CU):
+//   x    bf16 [28*28] + zero pad                                     1600
+//   a1   26x26 px x 32 ch bf16 (a1_off swizzle)                     43264
+//   zero 512 B: target of the dgrad reads whose dz2 row is outside the image
+//   dz2  24 rows x 26 px x 64 ch bf16; px 24, 25 of every row are zero, so a dgrad read
+//        that runs past either column edge lands on a zero pixel (col -1 of row r is px 25
+//        of row r-1; row -1 is the zero block)                        79872
+//   W2^T [tap][ci][co] bf16, 16-B chunk c of row (tap, ci) stored at c ^ ((ci >> 1) & 7)
+//        (conflict-free B-fragment reads)                             36864
+//   lut  bf16 of the normalised pixel value for each byte               512
+//   red  fp32 reduction scratch, aliases a1 (only used after the last image)
 constexpr int BWD_THREADS = 512;
-constexpr int DZW = 28;                         // dz2 image padded by 2 on every side
-constexpr int B_XS = 0;                         // bf16 x [784] + zero pad 1600
-constexpr int B_A1 = 1600;                      // a1 image              43264
-constexpr int B_DZ = B_A1 + P1 * 64;            // padded dz2 image      100352
-constexpr int B_RED = B_DZ + DZW * DZW * 128;   // fp32 reduction scratch
+constexpr int DS = 26;                          // dz2 row stride in pixels (24 + 2 zero)
+constexpr int B_XS = 0;
+constexpr int B_A1 = 1664;
+constexpr int B_Z0 = B_A1 + P1 * 64;            // 44928
+constexpr int B_DZ = B_Z0 + 512;                // 45440 (128-B aligned)
+constexpr int B_W2 = B_DZ + H2 * DS * 128;      // 125312
+constexpr int B_LUT = B_W2 + 9 * C1 * C2 * 2;   // normalize LUT: 256 x bf16    512
+constexpr int B_TOTAL = B_LUT + 512;            // 162688
+constexpr int B_RED = B_A1;
 constexpr int RED_DB2 = 0;                      // [8 waves][64]
 constexpr int RED_DW1 = RED_DB2 + 8 * C2;       // [4 waves][32 ci][16 taps] (tap 9 = bias)
 constexpr int RED_N = RED_DW1 + 4 * C1 * 16;    // 2560 floats
-constexpr int B_MK = B_RED + RED_N * 4;         // relu'(a1) bitmask: u32 [676] (bit = ci)
-constexpr int B_TOTAL = B_MK + P1 * 4;           // 158160 B -> 1 workgroup / CU
+static_assert(B_TOTAL <= 163840 && RED_N * 4 <= P1 * 64, "cnn_bwd LDS carve");
+static_assert(B_A1 % 128 == 0 && B_Z0 % 128 == 0 && B_DZ % 128 == 0 && B_W2 % 128 == 0,
+              "128-B aligned images (the dgrad address ORs a 7-bit swizzle into them)");
 constexpr int SL_DB2 = C2 * 9 * C1;             // 18432
 constexpr int SL_DW1 = SL_DB2 + C2;             // 18496
 constexpr int SL_DB1 = SL_DW1 + C1 * 9;         // 18784
 static_assert(SL_DB2 == CNN_CONV_SLAB_DB2 && SL_DW1 == CNN_CONV_SLAB_DW1 &&
               SL_DB1 == CNN_CONV_SLAB_DB1 && SL_DB1 + C1 == CNN_CONV_SLAB, "conv slab layout");
 
-// dz2 padded image: pixel (r, c) in [0,28)^2 holds dz2[r-2][c-2] (0 on the border), 128 B,
-// 16-B chunk XOR (2r + c) & 7: dgrad row reads conflict-free, wgrad transposed reads 2-way.
-__device__ __forceinline__ int dzp_off(int r, int c, int byte) {
-  return (r * DZW + c) * 128 + ((((byte >> 4) ^ ((2 * r + c) & 7))) << 4) + (byte & 15);
-}
+// dz2 image: pixel (r, c), 16-B chunk ch at ((ch + 4r + c) & 7) -- a rotation, so the
+// dgrad read address is two VALU ops per (tile, tap) (see dgrad_pass), and one step along
+// the dgrad's 28-wide virtual pixel grid (including 27 -> 0 of the next row: 4 - 27 = 1
+// mod 8) always advances the rotation by 1.  Conflict-free for the dgrad ds_read_b128 rows
+// and the scatter's window writes, 1.67-way for the wgrad ds_read_b64_tr_b16 columns
+// (tools/lds_bank_model.py).
+constexpr int W2_CHUNKS = 9 * C1 * C2 * 2 / 16;   // 2304 16-B chunks of W2^T
+constexpr int W2_PER_T = (W2_CHUNKS + BWD_THREADS - 1) / BWD_THREADS;   // 5
 
-// Stage one image into LDS: x (bf16, zero-padded), dz2 (expanded from the pooled gradient
-// and the argmax|positive mask), accumulate the conv2 bias gradient, then recompute
-// a1 = relu(conv1(x)) into its LDS image (cheaper than a 43 KB/image HBM round trip).
-// Every global load of the image is issued before the first LDS store.
+// Stage one image into LDS, ordered so that nothing waits for a load it does not need:
+//   1. issue every global load: x and the conv1 weights first, then (the workgroup's first
+//      image) W2^T, then dpool / pmask -- vmcnt retires in order;
+//   2. first image: build the 256-entry normalize LUT (exact torchvision arithmetic, bf16)
+//      and zero the dz2 pad pixels while the loads are in flight, then store W2^T, barrier;
+//   3. x -> bf16 through the LUT, barrier, conv1 recompute a1 = relu(conv1(x)) (needs only x
+//      and the conv1 weights: it runs while dpool / pmask are still arriving);
+//   4. the maxpool-backward scatter of dz2 (+ the conv2 bias gradient).
+// The caller's barrier ends the staging.  FIRST is a template flag so no runtime branch
+// joins the live W2^T registers (they spill).
+template <bool first>
 __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_t* __restrict__ xg,
                                                const bf16* __restrict__ dpool,
                                                const uint8_t* __restrict__ pmask,
                                                const float* __restrict__ w1,
-                                               const float* __restrict__ b1, bool first,
-                                               float (&db2p)[8]) {
+                                               const float* __restrict__ b1,
+                                               const bf16* __restrict__ w2t, float (&db2p)[8]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;
   bf16* xs = reinterpret_cast<bf16*>(smem + B_XS);
+  bf16* lut = reinterpret_cast<bf16*>(smem + B_LUT);
   char* a1s = smem + B_A1;
-  char* dzs = smem + B_DZ;
+  // ---- 1. loads
   uint32_t xw = 0;
   if (tid < 196) xw = reinterpret_cast<const uint32_t*>(xg + (int64_t)img * 784)[tid];
-  const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT);
-  const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT);
-  uint4 d[3];
-  uint2 mk[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int it = tid + k * BWD_THREADS;
-    if (it < PP * 8) {
-      d[k] = dpv[it];
-      mk[k] = mkv[it];
-    }
-  }
-  // conv1 operands, issued together with the image loads (unconditional clamped loads
-  // + selects: no per-load branch / wait)
   float w1v[2][4];
   int toff[4];
 #pragma unroll
@@ -286,46 +311,109 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
-  if (threadIdx.x == 0) PDM_STAMP_VAL(11, PDM_CLOCK());
-  // First image of the workgroup: zero the 2-pixel border of the padded dz2 image (never
-  // written afterwards) while the loads are in flight.  The 24x24 interior needs no
-  // clearing: the window writes below cover every interior pixel exactly once.
+  uint4 wv[W2_PER_T];
   if (first) {
-    for (int i = tid; i < 208 * 8; i += BWD_THREADS) {
-      const int pix = i >> 3;
-      int r, c;
-      if (pix < 112) {                    // rows 0, 1, 26, 27
-        r = pix / DZW;
-        c = pix - r * DZW;
-        r = r < 2 ? r : r + 24;
-      } else {                            // columns 0, 1, 26, 27 of rows 2..25
-        const int q = pix - 112;
-        r = 2 + (q >> 2);
-        c = (q & 3) < 2 ? (q & 3) : (q & 3) + 24;
-      }
-      *reinterpret_cast<uint4*>(dzs + (r * DZW + c) * 128 + (i & 7) * 16) = make_uint4(0, 0, 0, 0);
-    }
+#pragma unroll
+    for (int k = 0; k < W2_PER_T; ++k)
+      wv[k] = reinterpret_cast<const uint4*>(w2t)[min(tid + k * BWD_THREADS, W2_CHUNKS - 1)];
   }
+  const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT);
+  const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT);
+  uint4 d[3];
+  uint2 mk[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {   // clamped unconditional loads: no divergent branch for the
+    const int it = min(tid + k * BWD_THREADS, PP * 8 - 1);   // live W2^T registers to span
+    d[k] = dpv[it];
+    mk[k] = mkv[it];
+  }
+  // the arithmetic below stays behind the loads (hipcc otherwise hoists it above them and
+  // delays the first HBM request)
+  __builtin_amdgcn_sched_barrier(0);
+  if (threadIdx.x == 0) PDM_STAMP_VAL(11, PDM_CLOCK());
+  // ---- 2. LUT + pad zeroing (first image; both persist across the workgroup's images)
+  if (first) {
+    if (tid >= 256) lut[tid - 256] = to_bf16(pdm_normalize(tid - 256));
+    // zero pixels: columns 24, 25 of every dz2 row and the 4-pixel zero block
+    for (int i = tid; i < (2 * H2 + 4) * 8; i += BWD_THREADS) {
+      const int pix = i >> 3;
+      const int off = pix < 2 * H2 ? B_DZ + ((pix >> 1) * DS + 24 + (pix & 1)) * 128
+                                   : B_Z0 + (pix - 2 * H2) * 128;
+      *reinterpret_cast<uint4*>(smem + off + (i & 7) * 16) = make_uint4(0, 0, 0, 0);
+    }
+    // W2^T image before the barrier: its 20 registers must not live across it (hipcc spills
+    // them there).  Its loads precede dpool / pmask, so this waits for them only.  The
+    // clamped duplicate chunks rewrite the last chunk with the same value.
+#pragma unroll
+    for (int k = 0; k < W2_PER_T; ++k) {
+      const int it = min(tid + k * BWD_THREADS, W2_CHUNKS - 1);
+      const int row = it >> 3, ch = it & 7;
+      *reinterpret_cast<uint4*>(smem + B_W2 + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4)) = wv[k];
+    }
+    __syncthreads();   // LUT + W2^T ready (dpool / pmask keep flying)
+  }
+  // ---- 3. x through the LUT, conv1 recompute
   if (tid < 196) {
-    bf16x4 v = {to_bf16(pdm_normalize(xw & 0xff)), to_bf16(pdm_normalize((xw >> 8) & 0xff)),
-                to_bf16(pdm_normalize((xw >> 16) & 0xff)), to_bf16(pdm_normalize(xw >> 24))};
+    bf16x4 v = {lut[xw & 0xff], lut[(xw >> 8) & 0xff], lut[(xw >> 16) & 0xff], lut[xw >> 24]};
     reinterpret_cast<bf16x4*>(xs)[tid] = v;
   } else if (tid < 200) {
     reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};
   }
+  bf16x4 w1f[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
+  __syncthreads();
+  if (threadIdx.x == 0) PDM_STAMP_VAL(13, PDM_CLOCK());
+  // conv1 recompute: D[co][pixel] on mfma_f32_16x16x16_bf16 (same math as cnn_fwd), over
+  // tiles of 16 "virtual pixels" V = 28y + x of the 28-wide x image (x = 26, 27 and y >= 26
+  // computed and dropped): V is the pixel's own x-image index, x & 3 == lane & 3, so the
+  // operand reads are V + a per-lane tap offset and the a1 store is (V - 2y) * 64 + a
+  // per-lane constant.  46 tiles (48 slots) over 8 waves = 6 per wave, every x read of the
+  // 6 tiles issued before their MFMAs.
+  constexpr int TPW = 6;
+  int tb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tb[j] = toff[j] == IMG * IMG ? 0 : toff[j];   // w = 0 there
+  const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);   // mt = 0; mt = 1: ^ 32
+  bf16x4 bx[TPW];
+  int vv[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    vv[k] = (wave + 8 * k) * 16 + i16;
+    const int vc = min(vv[k], IMG * H1 - 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bx[k][j] = xs[vc + tb[j]];
+  }
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int y = vv[k] / IMG, x = vv[k] - y * IMG;
+    const bool ok = y < H1 && x < H1;
+    const int ab = (vv[k] - 2 * y) * 64 + a1c;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
+      bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
+                  to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
+      if (ok) *reinterpret_cast<bf16x4*>(a1s + (ab ^ (32 * mt))) = o;
+    }
+  }
+  if (threadIdx.x == 0) PDM_STAMP_VAL(14, PDM_CLOCK());
+  // ---- 4. the dz2 scatter
   // maxpool backward as whole-window writes: item (pooled pixel pp, 8-channel chunk ch)
   // builds the 16-B chunk of each of the window's 4 pixels (the pooled gradient at the
   // channel's argmax position if it was > 0, zero elsewhere) and stores 4 x 16 B.
-  // For window pos s = 2dy + dx the padded pixel is base + (dy*28 + dx) and its chunk
-  // swizzle (2r + c) & 7 is (b0 + s) & 7.
+  // For window pos s = 2dy + dx the pixel is (2py + dy, 2px + dx), rotation 4(2py + dy) +
+  // 2px + dx.
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int it = tid + k * BWD_THREADS;   // it & 7 == tid & 7: fixed channel chunk
     if (it < PP * 8) {
       const int pp = it >> 3, ch = it & 7;
       const int py = pp / HP, px = pp - py * HP;
-      const int base = ((2 * py + 2) * DZW + 2 * px + 2) * 128;
-      const int b0 = 4 * py + 2 * px + 6;
+      const int base = B_DZ + ((2 * py) * DS + 2 * px) * 128;
+      const int b0 = 2 * px + ch;                 // + 4 (2py + dy) + dx: 8py drops mod 8
       const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
       const uint32_t mw[2] = {mk[k].x, mk[k].y};
       uint32_t sel[8];                       // per channel: window position, or 4 if <= 0
@@ -346,179 +434,153 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
           ow[q] = (sel[2 * q] == (uint32_t)sw ? (w & 0xffffu) : 0u) |
                   (sel[2 * q + 1] == (uint32_t)sw ? (w & 0xffff0000u) : 0u);
         }
-        const int off = base + (sw >> 1) * (DZW * 128) + (sw & 1) * 128 + ((ch ^ ((b0 + sw) & 7)) << 4);
-        *reinterpret_cast<uint4*>(dzs + off) = o;
+        const int off = base + (sw >> 1) * (DS * 128) + (sw & 1) * 128 +
+                        (((b0 + 4 * (sw >> 1) + (sw & 1)) & 7) << 4);
+        *reinterpret_cast<uint4*>(smem + off) = o;
       }
     }
   }
   if (threadIdx.x == 0) PDM_STAMP_VAL(12, PDM_CLOCK());
   if (threadIdx.x == 448) PDM_STAMP_VAL(15, PDM_CLOCK());
-  bf16x4 w1f[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
-  __syncthreads();
-  if (threadIdx.x == 0) PDM_STAMP_VAL(13, PDM_CLOCK());
-  // conv1 recompute: D[co][pixel] on mfma_f32_16x16x16_bf16 (same math as cnn_fwd).
-  // 43 pixel tiles over 8 waves = 6 per wave (the last round clamps), every x read of
-  // the 6 tiles issued before their MFMAs.
-  constexpr int NT1 = (P1 + 15) / 16;                      // 43
-  constexpr int TPW = (NT1 + BWD_THREADS / 64 - 1) / (BWD_THREADS / 64);   // 6
-  bf16x4 bx[TPW];
-  int ty[TPW], tx[TPW];
-#pragma unroll
-  for (int k = 0; k < TPW; ++k) {
-    const int nt = min(wave + 8 * k, NT1 - 1);
-    const int P = min(nt * 16 + i16, P1 - 1);
-    ty[k] = P / H1;
-    tx[k] = P - ty[k] * H1;
-    const int xb = ty[k] * IMG + tx[k];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bx[k][j] = xs[toff[j] == IMG * IMG ? IMG * IMG : xb + toff[j]];
-  }
-#pragma unroll
-  for (int k = 0; k < TPW; ++k) {
-    const int nt = wave + 8 * k;
-    const bool ok = nt < NT1 && nt * 16 + i16 < P1;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-      bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
-                  to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        bits |= (from_bf16(o[r]) > 0.f ? 1u : 0u) << (16 * mt + 4 * g + r);
-      if (ok) *reinterpret_cast<bf16x4*>(a1s + a1_off(ty[k], tx[k], 32 * mt + 8 * g)) = o;
-    }
-    // relu' bitmask of the pixel: OR the 4 lane groups' channel bits
-    bits |= __shfl_xor(bits, 16, 64);
-    bits |= __shfl_xor(bits, 32, 64);
-    if (g == 0 && ok) reinterpret_cast<uint32_t*>(smem + B_MK)[nt * 16 + i16] = bits;
-  }
-  if (threadIdx.x == 0) PDM_STAMP_VAL(14, PDM_CLOCK());
 }
 
-// conv2 input gradient for MTP a1 pixel tiles {tile0 + 4k} of the staged image, fused with
-// relu'(a1) and the conv1 weight/bias gradient (accumulated into acc1).
+// conv2 input gradient for MTP tiles {tile0 + 4k} of 16 virtual pixels V = 28y + x (the
+// 28-wide x-image grid; x = 26, 27 and y >= 26 are computed on garbage and dropped by the
+// epilogue), fused with relu'(a1) and the conv1 weight/bias gradient (into acc1).
 //   da1[p][ci] = sum_tap sum_co dz2[p - tap][co] * W2[co][tap][ci]
-// 18 straight-line (tap, K-half) steps; each W2^T fragment is loaded 4 steps ahead into its
-// own register and the dz2 A fragments one step ahead (double buffer).  Tiles past the
-// image (>= 43) compute on clamped pixels and are discarded by the epilogue.
-template <int MTP, int PF>
-__device__ __forceinline__ void dgrad_pass(const char* dzs, const uint32_t* mks, const bf16* xs,
-                                           const bf16* w2t, int tile0, f32x4 (&acc1)[2],
-                                           unsigned long long& t_mf, unsigned long long& t_ep) {
+// 18 straight-line (tap, K-half) steps; the dz2 A fragments and the W2^T B fragments (both
+// LDS) are read PFD steps ahead.  Address of the A read of tile k at tap (ky, kx), K-half kh:
+//   ((gs[k] - 16(4ky + kx)) & 0x70 | rb[k][ky]) ^ 64kh,  immediate ((2-ky)*DS + 2-kx) * 128
+// where rb is the tile's row base (or the zero block for a dz2 row outside the image) and
+// gs = 16(g + 4y + x) seeds the rotation swizzle.
+template <int MTP, int PFD>
+__device__ __forceinline__ void dgrad_pass(const char* smem, int tile0, const int (&ka1)[4],
+                                           f32x4 (&acc1)[2], unsigned long long& t_mf,
+                                           unsigned long long& t_ep) {
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   const unsigned long long c0 = PDM_CLOCK();
-  // opaque zero offset per pass: the W2^T loads must not be hoisted out of the pass loop.
-  // (Laundering the pointer itself would turn them into flat loads, which also count on
-  // lgkmcnt and make every LDS wait drain the in-flight global prefetch.)
-  int wz = 0;
-  asm volatile("" : "+s"(wz));
-  const bf16* w2l = w2t + wz;
-  auto wfrag = [&](int t, int kh, int nt) {
-    return *reinterpret_cast<const bf16x8*>(w2l + (t * C1 + nt * 16 + i16) * C2 + 32 * kh + 8 * g);
-  };
-  int dbase[MTP], s0[MTP];
+  int rb[MTP][3], gs[MTP];
 #pragma unroll
   for (int k = 0; k < MTP; ++k) {
-    const int P = min((tile0 + 4 * k) * 16 + i16, P1 - 1);
-    const int y = P / H1, x = P - y * H1;
-    dbase[k] = ((y + 2) * DZW + x + 2) * 128;
-    s0[k] = 2 * y + x + 6;
+    const int v = (tile0 + 4 * k) * 16 + i16;
+    const int y = v / IMG, x = v - y * IMG;
+    const int a0 = B_DZ + ((y - 2) * DS + x - 2) * 128;
+    const int zb = B_Z0 + (x & 1) * 128;       // same bank parity as the real pixel
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+      rb[k][ky] = ((unsigned)(y - ky) < (unsigned)H2) ? a0 : zb - (2 - ky) * DS * 128;
+    gs[k] = (g + 4 * y + x) << 4;
   }
+  const int wl0 = B_W2 + i16 * 128 + ((g ^ ((i16 >> 1) & 7)) << 4);
+  auto read_step = [&](int tk, bf16x8 (&a)[MTP], bf16x8 (&w)[2]) {
+    const int tap = tk >> 1, kh = tk & 1;
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const int sk16 = (4 * ky + kx) << 4;
+    const int off = ((2 - ky) * DS + (2 - kx)) * 128;
+#pragma unroll
+    for (int k = 0; k < MTP; ++k) {
+      int ad = ((gs[k] - sk16) & 0x70) | rb[k][ky];
+      if (kh) ad ^= 64;
+      a[k] = *reinterpret_cast<const bf16x8*>(smem + ad + off);
+    }
+    const int wl = kh ? (wl0 ^ 64) : wl0;
+    w[0] = *reinterpret_cast<const bf16x8*>(smem + wl + tap * 4096);
+    w[1] = *reinterpret_cast<const bf16x8*>(smem + wl + tap * 4096 + 2048);
+  };
+  // epilogue operands.  Lane (g, ctap = i16) holds the dgrad outputs of pixels V0 + r,
+  // V0 = 16 tile + 4g (a run of 4 in one row: 28 = 7 x 4) for channels i16 and 16 + i16.
+  // conv1 wgrad B operand: x[V0 + r + tap offset]; relu'(a1) from the a1 image at
+  // (V0 - 2y) * 64 + ka1[r] (^ 32 for channel 16 + i16), where x & 3 == r fixes the swizzle.
+  const int ctap = i16;
+  const int cky = ctap / 3, ckx = ctap - 3 * cky;
+  const int xoff = (ctap < 9) ? (cky * IMG + ckx) : 0;   // taps >= 9: any finite value
+  const bf16* xs = reinterpret_cast<const bf16*>(smem + B_XS);
+  bf16x4 bx[MTP];
+  short av[MTP][4][2];
+  bool vhi[MTP];
+  auto read_ep = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < MTP; ++k) {
+      const int v0 = (tile0 + 4 * k) * 16 + 4 * g;
+      const int y = v0 / IMG, x0 = v0 - y * IMG;
+      const bool vt = y < H1;
+      vhi[k] = vt && x0 < 24;                   // pixels x0 + 2, x0 + 3 inside the row
+      const int vc = vt ? v0 : 0;
+      const int pb = vt ? B_A1 + (v0 - 2 * y) * 64 : B_Z0;   // zero block: relu' = 0
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bx[k][r] = xs[vc + r + xoff];
+        av[k][r][0] = *reinterpret_cast<const short*>(smem + pb + ka1[r]);
+        av[k][r][1] = *reinterpret_cast<const short*>(smem + pb + (ka1[r] ^ 32));
+      }
+    }
+  };
   f32x4 acc[MTP][2];
 #pragma unroll
   for (int k = 0; k < MTP; ++k) acc[k][0] = acc[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 w[18][2];
+  bf16x8 a[PFD + 1][MTP], w[PFD + 1][2];
 #pragma unroll
-  for (int tk = 0; tk < PF; ++tk) {
-    w[tk][0] = wfrag(tk >> 1, tk & 1, 0);
-    w[tk][1] = wfrag(tk >> 1, tk & 1, 1);
-  }
-  auto read_a = [&](int tk, bf16x8 (&a)[MTP]) {
-    const int t = tk >> 1, kh = tk & 1;
-    const int ky = t / 3, kx = t - 3 * ky;
-    const int toffb = (ky * DZW + kx) * 128;
-    const int gk = g + 4 * kh;
-    const int sk = 2 * ky + kx;
-#pragma unroll
-    for (int k = 0; k < MTP; ++k)
-      a[k] = *reinterpret_cast<const bf16x8*>(dzs + dbase[k] - toffb +
-                                              ((gk ^ ((s0[k] - sk) & 7)) << 4));
-  };
-  bf16x8 a[2][MTP];
-  read_a(0, a[0]);
+  for (int tk = 0; tk < PFD; ++tk) read_step(tk, a[tk], w[tk]);
 #pragma unroll
   for (int tk = 0; tk < 18; ++tk) {
-    __builtin_amdgcn_sched_barrier(0);   // keep each step's loads where they are issued
-    if (tk + PF < 18) {
-      w[tk + PF][0] = wfrag((tk + PF) >> 1, (tk + PF) & 1, 0);
-      w[tk + PF][1] = wfrag((tk + PF) >> 1, (tk + PF) & 1, 1);
-    }
-    if (tk + 1 < 18) read_a(tk + 1, a[(tk + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);   // keep each step's reads where they are issued
+#if PDM_ABL == 3
+    if (tk + PFD == 18) read_ep();   // timing ablation: no operand reads in the step loop
+#else
+    if (tk + PFD < 18) read_step(tk + PFD, a[(tk + PFD) % (PFD + 1)], w[(tk + PFD) % (PFD + 1)]);
+    else if (tk + PFD == 18) read_ep();
+#endif
+    // the reads go out before this step's MFMAs (hipcc otherwise sinks them below the
+    // MFMAs and the read-ahead shrinks to ~1 step: lgkmcnt(7) instead of lgkmcnt(12))
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = tk % (PFD + 1);
 #pragma unroll
     for (int k = 0; k < MTP; ++k) {
-      acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][0], acc[k][0], 0, 0, 0);
-      acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tk & 1][k], w[tk][1], acc[k][1], 0, 0, 0);
+      acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][k], w[s][0], acc[k][0], 0, 0, 0);
+      acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][k], w[s][1], acc[k][1], 0, 0, 0);
     }
   }
   const unsigned long long c1 = PDM_CLOCK();
   t_mf += c1 - c0;
-  // epilogue per tile: relu'(a1) bitmask -> dz1 (bf16) -> conv1 wgrad on
-  // mfma_f32_16x16x16_bf16 (M = ci, N = tap 0..8 / 9 = ones -> bias, K = pixels); the
-  // dgrad accumulator (lane: ci = 16nt + i16, pixels 4g + r) is already its A operand.
-  const int ctap = i16;
-  const int cky = ctap / 3, ckx = ctap - 3 * cky;
-  const int xoff = (ctap < 9) ? (cky * IMG + ckx) : IMG * IMG;
+  // epilogue per tile: relu'(a1) -> dz1 (bf16) -> conv1 wgrad on mfma_f32_16x16x16_bf16
+  // (M = ci, N = tap 0..8 / 9 = ones -> bias, K = pixels); the dgrad accumulator
+  // (lane: ci = 16nt + i16, pixels 4g + r) is already its A operand.  a1 > 0 is tested on
+  // the bf16 bits as a signed 16-bit integer.
   const bf16 one = to_bf16(1.f);
 #pragma unroll
   for (int k = 0; k < MTP; ++k) {
-    const int P0 = (tile0 + 4 * k) * 16 + 4 * g;
-    const int y0 = P0 / H1, x0 = P0 - y0 * H1;
-    bf16x4 bx;
-    uint32_t mw[4];
-    bool valid[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool wrap = x0 + r >= H1;
-      const int yr = wrap ? y0 + 1 : y0, xr = wrap ? x0 + r - H1 : x0 + r;
-      valid[r] = P0 + r < P1;
-      const int yc = valid[r] ? yr : 0, xc = valid[r] ? xr : 0;
-      const int xi = (ctap < 9) ? yc * IMG + xc + xoff : IMG * IMG;
-      bx[r] = xs[xi];
-      mw[r] = mks[yc * H1 + xc];
-    }
-    if (ctap == 9) bx = bf16x4{one, one, one, one};
+    const bf16x4 b = (ctap == 9) ? bf16x4{one, one, one, one} : bx[k];
     bf16x4 az[2];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        az[nt][r] = to_bf16((valid[r] && ((mw[r] >> (16 * nt + i16)) & 1u)) ? acc[k][nt][r] : 0.f);
+        az[nt][r] = to_bf16((av[k][r][nt] > 0 && (r < 2 || vhi[k])) ? acc[k][nt][r] : 0.f);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
-      acc1[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az[nt], bx, acc1[nt], 0, 0, 0);
+      acc1[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(az[nt], b, acc1[nt], 0, 0, 0);
   }
   t_ep += PDM_CLOCK() - c1;
 }
 
 // Work split (per image, after the staged load): waves 0-3 run the conv2 wgrad (18 (tap,
-// ci-tile) pairs), waves 4-7 the dgrad over 48 tile slots (43 real) in passes of DG_MTP.
-// PDM_DG_SPLIT=16 moves dgrad tiles 0..15 onto the wgrad waves when a workgroup has one
-// image.  Measured on MI355X (B=256, tools/kbench.py): split 0 / MTP 6 = 24.8 us, split 16 /
-// MTP 8 = 24.8 us, split 16 / MTP 4 = 27.3 us, split 0 / MTP 4 = 27.4 us: the balance does not
-// matter, the MFMAs per dgrad step do (the kernel is latency-bound at 2 waves per SIMD).
-#ifndef PDM_DG_SPLIT
-#define PDM_DG_SPLIT 0
+// ci-tile) pairs), waves 4-7 the dgrad over 48 tile slots (46 of the 28-wide virtual grid)
+// in passes of DG_MTP tiles with operands read DG_PFD steps ahead; with one image per
+// workgroup the wgrad waves run the third dgrad pass after their wgrad.
+#ifndef PDM_ABL
+#define PDM_ABL 0     // diagnostic builds only: 1 skip wgrad, 2 skip dgrad, 3 dgrad without reads
 #endif
-constexpr int DG_SPLIT = PDM_DG_SPLIT;   // dgrad tiles done by the wgrad waves (0 or 16)
 #ifndef PDM_DG_MTP
-#define PDM_DG_MTP 6
+#define PDM_DG_MTP 4
+#endif
+#ifndef PDM_DG_PFD
+#define PDM_DG_PFD 2
 #endif
 constexpr int DG_MTP = PDM_DG_MTP;       // tiles per dgrad pass on waves 4-7
+constexpr int DG_PFD = PDM_DG_PFD;       // read-ahead distance in (tap, K-half) steps
+static_assert(DG_MTP == 4, "dgrad passes: 3 x 4 tiles per wave (the wgrad waves take pass 2 when "
+              "a workgroup has one image)");
+static_assert(DG_PFD * (DG_MTP + 2) <= 15, "in-flight LDS reads must fit lgkmcnt");
 
 __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     const uint8_t* __restrict__ xg, const float* __restrict__ w1, const float* __restrict__ b1,
@@ -532,26 +594,22 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
   float* red = reinterpret_cast<float*>(smem + B_RED);
-  const bf16* xs = reinterpret_cast<const bf16*>(smem + B_XS);
   const char* a1s = smem + B_A1;
-  const char* dzs = smem + B_DZ;
-  const uint32_t* mks = reinterpret_cast<const uint32_t*>(smem + B_MK);
   float* out = slab + (int64_t)blockIdx.x * CONV_SLAB;
   float db2p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   unsigned long long t_mf = 0, t_ep = 0;
+  // relu'(a1) read offsets of channel i16 at pixel x with x & 3 == r (a1_off swizzle)
+  int ka1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ka1[r] = r * 64 + ((((2 * i16) >> 4) ^ r) << 4) + ((2 * i16) & 15);
   PDM_STAMP(0);
 
   if (wave < 4) {
     // ===== conv2 weight gradient: (tap, ci-tile) pairs {w, w+4, ...} x all 4 co tiles =====
     // K = output pixels in chunks of 8 along a row (24 = 3 chunks): lane group g of k-step
-    // ks takes chunk 4ks+g; its lane q reads pixels x = col0+q and x+4 (col0 % 8 == 0), so
-    // every swizzle term below is a per-lane constant and each read costs one add.
-    f32x4 acc[5][4];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // ks takes chunk 4ks+g; its lane q reads pixels x = col0+q and x+4 (col0 % 8 == 0).
+    f32x4 acc[5][4];   // zeroed after the first image's staging (not live through it)
     const bool five = wave < 2;  // 18 pairs over 4 waves: 5,5,4,4 (+1 discarded on 2,3)
     int cpair[5];
 #pragma unroll
@@ -562,91 +620,135 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
       cpair[pi] = (ky * H1 + kx) * 64 + (((2 * nt + (pq >> 1)) ^ ((q + kx) & 3)) << 4) + 8 * (pq & 1);
     }
     const int u8b = 8 * (pq & 1);
-    auto wgrad_image = [&]() {
-#pragma unroll 2
-      for (int ks = 0; ks < P2 / 32; ++ks) {
-        const int c8 = ks * 4 + g;
-        const int row = c8 / 3;
-        const int x = (c8 - 3 * row) * 8 + q;
-        const int abase = (row * H1 + x) * 64;
-        const int dbase = ((row + 2) * DZW + x + 2) * 128 + u8b;
-        const int t = (((pq >> 1) ^ ((2 * row + x + 6) & 7)) << 4);
-        bf16x8 A[4];
+    // Operand addresses of k-step ks = 3m + j: lane group g reads dz2/a1 row 4m + r_j,
+    // columns 8c_j + q (and + 4), with 4j + g = 3r_j + c_j.  The dz2 rotation (4 row + x)
+    // mod 8 does not depend on m, so every address is a per-lane base of (j, fragment) plus
+    // the immediate m * (4 rows): no address arithmetic inside the k loop.
+    int abA[3][4], abA2[3][4], abB[3][5];
+    // (filled after the first image's loads are issued: 51 VALU-computed registers that
+    // would otherwise delay the wgrad waves' share of the staging loads)
+    auto setup_addr = [&]() __attribute__((always_inline)) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          A[mt] = cat_tr(lds_tr16(dzs + dbase + ((32 * mt) ^ t)),
-                         lds_tr16(dzs + dbase + 512 + ((32 * mt) ^ t ^ 64)));
+    for (int j = 0; j < 3; ++j) {
+      const int v = 4 * j + g, rj = v / 3, xj = (v - 3 * rj) * 8 + q;
+      const int dbase = B_DZ + (rj * DS + xj) * 128 + u8b;
 #pragma unroll
-        for (int pi = 0; pi < 5; ++pi) {   // waves 2,3: pair 4 is a discarded duplicate
-          const bf16x8 Bv = cat_tr(lds_tr16(a1s + abase + cpair[pi]),
-                                   lds_tr16(a1s + abase + cpair[pi] + 256));
+      for (int mt = 0; mt < 4; ++mt) {
+        // chunk 2mt + (pq >> 1) rotated by (4 row + x); pixel x + 4 is rotated 4 further,
+        // i.e. its chunk offset is this one ^ 64
+        const int co = (((pq >> 1) + 4 * rj + xj + 2 * mt) & 7) << 4;
+        abA[j][mt] = dbase + co;
+        abA2[j][mt] = dbase + 512 + (co ^ 64);
+      }
+#pragma unroll
+      for (int pi = 0; pi < 5; ++pi) abB[j][pi] = B_A1 + (rj * H1 + xj) * 64 + cpair[pi];
+    }
+    };
+    auto rd_a = [&](int ks, int mt) __attribute__((always_inline)) {
+      const int j = ks % 3, m = ks / 3;
+      return cat_tr(lds_tr16(smem + abA[j][mt] + m * 4 * DS * 128),
+                    lds_tr16(smem + abA2[j][mt] + m * 4 * DS * 128));
+    };
+    auto rd_b = [&](int ks, int pi) __attribute__((always_inline)) {
+      const int j = ks % 3, m = ks / 3;
+      return cat_tr(lds_tr16(smem + abB[j][pi] + m * 4 * H1 * 64),
+                    lds_tr16(smem + abB[j][pi] + m * 4 * H1 * 64 + 256));
+    };
+    // software-pipelined over k-steps: region pi of step ks issues the reads of step ks+1
+    // (B fragment pi and A fragment pi) ahead of its 4 MFMAs, so every operand is one whole
+    // step (20 MFMAs) old when it is consumed
+    auto wgrad_image = [&]() __attribute__((always_inline)) {
+      bf16x8 A[2][4], Bv[2][5];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) A[0][mt] = rd_a(0, mt);
+#pragma unroll
+      for (int pi = 0; pi < 5; ++pi) Bv[0][pi] = rd_b(0, pi);
+      // compile-time k loop (hipcc leaves an 18-trip `#pragma unroll` loop rolled and then
+      // keeps the register arrays it indexes in scratch)
+      static_for<P2 / 32>([&](auto KS) __attribute__((always_inline)) {
+        constexpr int ks = decltype(KS)::value;
+        bf16x8 (&Ac)[4] = A[ks & 1];
+        bf16x8 (&Bc)[5] = Bv[ks & 1];
+        bf16x8 (&An)[4] = A[(ks + 1) & 1];
+        bf16x8 (&Bn)[5] = Bv[(ks + 1) & 1];
+#pragma unroll
+        for (int pi = 0; pi < 5; ++pi) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 1 < P2 / 32) {
+            Bn[pi] = rd_b(ks + 1, pi);
+            if (pi < 4) An[pi] = rd_a(ks + 1, pi);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)   // waves 2,3: pair 4 is a discarded duplicate
+            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ac[mt], Bc[pi], acc[pi][mt], 0, 0, 0);
+        }
+      });
+    };
+    // the accumulators persist across the workgroup's images; after the last image they
+    // are stored while the dgrad waves are still computing.  dW2[co][tap][ci]: rows
+    // co = 16mt + 4g + r, col ci = 16nt + i16
+    auto per_image = [&](auto first, int i, bool last) __attribute__((always_inline)) {
+      const int img = blockIdx.x * ipb + i;
+      if (img < B) bwd_load_image<decltype(first)::value>(smem, img, xg, dpool, pmask, w1, b1, w2t, db2p);
+      if constexpr (decltype(first)::value) setup_addr();
+      __syncthreads();
+      if constexpr (decltype(first)::value) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      PDM_STAMP(1);
+      if (img < B && PDM_ABL != 1) wgrad_image();   // PDM_ABL: timing ablations only
+      PDM_STAMP(2);
+      if (last) {
+#pragma unroll
+        for (int pi = 0; pi < 5; ++pi) {
+          if (pi == 4 && !five) break;
+          const int pair = wave + 4 * pi;
+          const int tap = pair >> 1, nt = pair & 1;
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
-            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mt], Bv, acc[pi][mt], 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + nt * 16 + i16] = acc[pi][mt][r];
         }
-      }
-    };
-    // dW2[co][tap][ci]: rows co = 16mt + 4g + r, col ci = 16nt + i16
-    auto store_wgrad = [&]() {
-#pragma unroll
-      for (int pi = 0; pi < 5; ++pi) {
-        if (pi == 4 && !five) break;
-        const int pair = wave + 4 * pi;
-        const int tap = pair >> 1, nt = pair & 1;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + nt * 16 + i16] = acc[pi][mt][r];
-      }
-    };
-    if (ipb == 1) {
-      // one image: wgrad, store it (frees its 80 accumulators), then dgrad tiles 0..15
-      const int img = blockIdx.x;
-      if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, true, db2p);
-      __syncthreads();
-      PDM_STAMP(1);
-      if (img < B) {
-        wgrad_image();
-        PDM_STAMP(2);
-        store_wgrad();
-        if (DG_SPLIT > 0) dgrad_pass<(DG_SPLIT > 0 ? DG_SPLIT / 4 : 1), 4>(dzs, mks, xs, w2t, wave, acc1, t_mf, t_ep);
-      } else {
-        store_wgrad();
-      }
-      PDM_STAMP(3);
-      __syncthreads();
-    } else {
-      // several images: the wgrad accumulators persist across them; dgrad is all on 4-7
-      for (int i = 0; i < ipb; ++i) {
-        const int img = blockIdx.x * ipb + i;
-        if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
-        __syncthreads();
-        PDM_STAMP(1);
-        if (img < B) wgrad_image();
         PDM_STAMP(3);
-        __syncthreads();
       }
-      store_wgrad();
-    }
+      // one image per workgroup: with its accumulators stored, this wave also takes the
+      // last dgrad pass (tiles 32 + wave + 4k), which balances the two wave groups (the
+      // wgrad's 360 MFMAs vs the dgrad's 432 + epilogues)
+      if constexpr (decltype(first)::value) {
+        if (ipb == 1 && img < B && PDM_ABL != 2)
+          dgrad_pass<DG_MTP, DG_PFD>(smem, 32 + wave, ka1, acc1, t_mf, t_ep);
+      }
+      __syncthreads();
+    };
+    // one image per workgroup (B <= CUs): straight-line code, nothing hoisted out of an
+    // image loop (hipcc would keep the loop-invariant addresses live and spill)
+    per_image(std::true_type{}, 0, ipb == 1);
+    for (int i = 1; i < ipb; ++i) per_image(std::false_type{}, i, i == ipb - 1);
   } else {
     // ===== conv2 input gradient + relu'(a1) + conv1 weight/bias gradient =====
     const int wd = wave - 4;
-    for (int i = 0; i < ipb; ++i) {
+    auto per_image = [&](auto first, int i) __attribute__((always_inline)) {
       const int img = blockIdx.x * ipb + i;
-      if (img < B) bwd_load_image(smem, img, xg, dpool, pmask, w1, b1, i == 0, db2p);
+      if (img < B) bwd_load_image<decltype(first)::value>(smem, img, xg, dpool, pmask, w1, b1, w2t, db2p);
       __syncthreads();
-      if (img < B) {
-        // tiles T0 + wd + 4j, j < (48 - T0) / 4, in passes of DG_MTP tiles; a rolled pass
-        // loop keeps one copy of the pass code and stops cross-pass scheduling
-        const int t0 = ipb > 1 ? 0 : DG_SPLIT;
-        const int n = (48 - t0) / 4;
+      if (img < B && PDM_ABL != 2) {
+        // tiles wd + 4j, j < 12, in passes of DG_MTP tiles; a rolled pass loop keeps one
+        // copy of the pass code and stops cross-pass scheduling
+        // (one image per workgroup: the wgrad waves take the last pass)
+        const int npass = ipb == 1 ? 12 / DG_MTP - 1 : 12 / DG_MTP;
 #pragma unroll 1
-        for (int ps = 0; ps * DG_MTP < n; ++ps)
-          dgrad_pass<DG_MTP, 4>(dzs, mks, xs, w2t, t0 + wd + 4 * DG_MTP * ps, acc1, t_mf, t_ep);
+        for (int ps = 0; ps < npass; ++ps)
+          dgrad_pass<DG_MTP, DG_PFD>(smem, wd + 4 * DG_MTP * ps, ka1, acc1, t_mf, t_ep);
       }
       __syncthreads();
-    }
+    };
+    per_image(std::true_type{}, 0);
+    for (int i = 1; i < ipb; ++i) per_image(std::false_type{}, i);
     if (tid == 256) {
       PDM_STAMP_VAL(8, t_mf);
       PDM_STAMP_VAL(9, t_ep);
@@ -654,7 +756,8 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     }
   }
   // conv1 weight/bias partials, acc1[nt]: rows ci = 16nt + 4g + r, col tap = i16.  Waves 4-7
-  // write their slot, waves 0-3 then add theirs (slot = wave & 3).
+  // write their slot, waves 0-3 then add theirs (slot = wave & 3).  (red aliases a1, which
+  // is dead once both wave groups have passed the last image barrier.)
   float* r1 = red + RED_DW1 + (wave & 3) * C1 * 16;
   if (wave >= 4) {
 #pragma unroll

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_cnn_bwd_exact.py tests/test_gpu_cnn.py > gpurun_out/t_cnn.log 2>&1 && \
+timeout -k 10 300 python -u tools/kbench.py 256 1024 8192 > gpurun_out/kbench.log 2>&1 && \
+PDM_EXT_PATH=build/stamps/_C.cpython-310-x86_64-linux-gnu.so timeout -k 10 120 python -u tools/stamps.py 256 > gpurun_out/stamps256.log 2>&1
+echo rc=$?
