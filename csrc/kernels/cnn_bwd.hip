@@ -43,8 +43,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 // ------------------------------------------------------------------ fc1_bwd
 constexpr int DW_TILES = FEAT / 64;  // 144
 constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
-constexpr int DX_COLS = 128;         // dX tile: 32 batch rows x 128 features per workgroup
-constexpr int DX_TILES = FEAT / DX_COLS;   // 72 = 8 XCDs x 9
+constexpr int DX_COLS = 384;         // dX tile: 32 batch rows x 384 features per workgroup
+constexpr int DX_TILES = FEAT / DX_COLS;   // 24 = 8 XCDs x 3
+constexpr int DX_FT = DX_COLS / 64;        // 16-feature sub-tiles per wave (6)
 constexpr int NXCD = 8;              // MI355X: workgroups are dealt round-robin to 8 XCDs
 static_assert(DX_TILES % NXCD == 0 && DW_TILES % NXCD == 0, "XCD-aware tile mapping");
 constexpr int HR_BLOCKS = (HEAD_SLAB + 63) / 64;   // head-slab reduction workgroups (23)
@@ -138,42 +139,44 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   }
 
   if (bid < DW_TILES + nd) {
-    // ---- dX tile: 32 batch rows x 128 features, K = 128 hidden ----
+    // ---- dX tile: 32 batch rows x 384 features, K = 128 hidden ----
     // Computed transposed, dpool^T[f][b] = W1^T[f][:] . dh^T[:][b]: the MFMA output lane then
     // holds 4 consecutive features of one batch row, stored as one 8-byte bf16x4.  Each wave
-    // owns 32 features x 32 rows; all operand loads of the wave are issued up front.
-    // XCD-aware: workgroup t runs on XCD t % 8 (DW_TILES is a multiple of 8), and every XCD
-    // owns 1/8 of the feature range, so each XCD's L2 holds only its 1/8 of W1^T.
+    // owns 96 features (6 sub-tiles) x 32 rows with every operand load (24 W1^T + 8 dh
+    // fragments) issued up front: at B = 256 the 192 tiles are one round of workgroups, each
+    // a single load burst (the earlier 576 tiles of 128 features ran ~2.25 latency-bound
+    // rounds per CU).  XCD-aware: workgroup t runs on XCD t % 8 (DW_TILES is a multiple of
+    // 8), and every XCD owns 1/8 of the feature range, so each XCD's L2 holds only its 1/8
+    // of W1^T.
     const int t = bid - DW_TILES;
     constexpr int TPX = DX_TILES / NXCD;                 // feature tiles per XCD
     const int xcd = t % NXCD, loc = t / NXCD;
     const int b0 = (loc / TPX) * 32;
-    const int f0 = (xcd * TPX + loc % TPX) * DX_COLS + wave * 32;
-    constexpr int FT = 2;
-    bf16x8 wa[FT][HID / 32], hb[2][HID / 32];
+    const int f0 = (xcd * TPX + loc % TPX) * DX_COLS + wave * (16 * DX_FT);
+    bf16x8 wa[DX_FT][HID / 32], hb[2][HID / 32];
 #pragma unroll
     for (int ks = 0; ks < HID / 32; ++ks) {
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
-        wa[ft][ks] = *reinterpret_cast<const bf16x8*>(
-            wf1t + (int64_t)(f0 + ft * 16 + i16) * HID + 32 * ks + 8 * g);
 #pragma unroll
       for (int bt = 0; bt < 2; ++bt)
         hb[bt][ks] = *reinterpret_cast<const bf16x8*>(
             dh + (int64_t)(b0 + bt * 16 + i16) * HID + 32 * ks + 8 * g);
+#pragma unroll
+      for (int ft = 0; ft < DX_FT; ++ft)
+        wa[ft][ks] = *reinterpret_cast<const bf16x8*>(
+            wf1t + (int64_t)(f0 + ft * 16 + i16) * HID + 32 * ks + 8 * g);
     }
     // keep every load above this point: the scheduler would otherwise interleave them
     // with the MFMAs behind per-load waits
     __builtin_amdgcn_sched_barrier(0);
-    f32x4 acc[FT][2];
+    f32x4 acc[DX_FT][2];
 #pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
+    for (int ft = 0; ft < DX_FT; ++ft)
 #pragma unroll
       for (int bt = 0; bt < 2; ++bt) acc[ft][bt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < HID / 32; ++ks)
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
+      for (int ft = 0; ft < DX_FT; ++ft)
 #pragma unroll
         for (int bt = 0; bt < 2; ++bt)
           acc[ft][bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ft][ks], hb[bt][ks], acc[ft][bt], 0, 0, 0);
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       const int row = b0 + bt * 16 + i16;
       if (row < B) {
 #pragma unroll
-        for (int ft = 0; ft < FT; ++ft) {
+        for (int ft = 0; ft < DX_FT; ++ft) {
           const bf16x4 o = {to_bf16(acc[ft][bt][0]), to_bf16(acc[ft][bt][1]),
                             to_bf16(acc[ft][bt][2]), to_bf16(acc[ft][bt][3])};
           *reinterpret_cast<bf16x4*>(dpool + (int64_t)row * FEAT + f0 + ft * 16 + 4 * g) = o;

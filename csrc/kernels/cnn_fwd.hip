@@ -27,7 +27,8 @@ constexpr int F_XS = 0;                       // bf16 x [28*28] + zero pad  1600
 constexpr int F_A1 = 1600;                    // bf16 a1 image              43264 B
 constexpr int F_PS = F_A1 + P1 * 64;          // bf16 pooled [144][64]      18432 B
 constexpr int F_MS = F_PS + PP * C2 * 2;      // u8 mask [144][64]          9216 B
-constexpr int F_TOTAL = F_MS + PP * C2;       // 72512 B -> 2 workgroups / CU
+constexpr int F_LUT = F_MS + PP * C2;         // bf16 normalize LUT [256]     512 B
+constexpr int F_TOTAL = F_LUT + 512;          // 73024 B -> 2 workgroups / CU
 
 template <bool TRAIN>
 __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
@@ -57,48 +58,47 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   const int64_t src = idx ? (int64_t)idx[row] : row;
   uint32_t xw = 0;
   if (tid < 196) xw = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];
-  if (tid == 0) ylab[img] = labels[src];
+  // the label is a per-lane (vector) load consumed at the very end: a uniform-address
+  // scalar load here made wave 0 wait for it (s_waitcnt lgkmcnt(0)) before issuing its
+  // weight loads, delaying the first barrier by ~1.7k cycles
+  int lab = 0;
+  if (tid == 64) {
+    int vz;   // a VGPR zero: keeps the load a vector load (a uniform address becomes s_load)
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+    lab = labels[src + vz];
+  }
   if (tid == 0) PDM_STAMP_VAL(8, PDM_CLOCK());   // image load issued
+  // normalize through a 256-entry LUT (exact torchvision arithmetic -- two IEEE divisions --
+  // once per byte value, not per pixel), built by the upper waves while the image is in
+  // flight and BEFORE they queue their 18 KB of conv2 weight loads (the TA queue would
+  // otherwise hold the LUT, and the barrier, back by ~2k cycles)
+  bf16* lut = reinterpret_cast<bf16*>(smem + F_LUT);
+  if (tid >= 256) lut[tid - 256] = to_bf16(pdm_normalize(tid - 256));
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();   // normalize LUT ready (the image load keeps flying)
 
   // conv1 as D[co][pixel] = W1[co][tap] . X[tap][pixel] on mfma_f32_16x16x16_bf16:
   // A = weights (lane row co = i16, k = taps 4g..4g+3, zero past tap 8), B = input
   // patches (lane col = pixel, k = taps); bias is the initial accumulator.
-  bf16x4 w1f[2];
+  // (the bf16 conversion of the weights happens after the barriers: converting here made
+  // every wave wait for its conv1 weight loads before the first barrier)
+  float w1v[2][4];
   int toff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int tap = 4 * g + j;
     toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;  // -> zero pad entry
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {   // clamped unconditional load + select (no branch/wait)
-      const float wv = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
-      w1f[mt][j] = to_bf16(tap < 9 ? wv : 0.f);
-    }
+    for (int mt = 0; mt < 2; ++mt)   // clamped unconditional load (no branch/wait)
+      w1v[mt][j] = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
   }
   f32x4 b1v[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
-  // conv2 B fragments for this wave's two n-tiles (co = 32*(wave&1) + 16*j + i16):
-  // lane l holds B[k = ci = 8g + e][n = co] = w2[co][tap][ci].  Issued after every load
-  // conv1 needs: global loads retire in order (vmcnt), so conv1 does not wait for these
-  // 18 KB per wave, which stream in while the image is normalised and conv1 runs.
-  const int nh = wave & 1;
-  float b2r[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) b2r[j] = b2[nh * 32 + j * 16 + i16];
-  bf16x8 wb[9][2];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      wb[t][j] = *reinterpret_cast<const bf16x8*>(
-          w2 + ((nh * 32 + j * 16 + i16) * 9 + t) * 32 + 8 * g);
-
   if (tid < 196) {
-    bf16x4 v = {to_bf16(pdm_normalize(xw & 0xff)), to_bf16(pdm_normalize((xw >> 8) & 0xff)),
-                to_bf16(pdm_normalize((xw >> 16) & 0xff)), to_bf16(pdm_normalize(xw >> 24))};
+    bf16x4 v = {lut[xw & 0xff], lut[(xw >> 8) & 0xff], lut[(xw >> 16) & 0xff], lut[xw >> 24]};
     reinterpret_cast<bf16x4*>(xs)[tid] = v;
     if (TRAIN) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[tid] = xw;
     if (tid == 0) PDM_STAMP_VAL(9, PDM_CLOCK());   // image landed
@@ -108,22 +108,69 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   __syncthreads();
   PDM_STAMP(1);
 
+  __builtin_amdgcn_sched_barrier(0);   // (hipcc hoists the conversion above the barrier)
+  // conv2 B fragments for this wave's two n-tiles (co = 32*(wave&1) + 16*j + i16):
+  // lane l holds B[k = ci = 8g + e][n = co] = w2[co][tap][ci].  Issued only now, once the
+  // image has landed: these 18 KB per wave (147 KB per CU, all L2 hits) queued in the L2
+  // ahead of the image's HBM request held the image back ~5k cycles; they stream in while
+  // conv1 runs.
+  const int nh = wave & 1;
+  float b2r[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b2r[j] = b2[nh * 32 + j * 16 + i16];
+  bf16x8 wb[9][2];
+  // issued 3 per conv1 tile below: all 18 at once filled the CU's TA queue (8 waves x 18 KB)
+  // and stalled every wave's conv1 issue behind them for ~2.3k cycles
+  auto load_wb = [&](int f) {   // fragments 3f .. 3f+2 of the 18 (tap, n-tile) pairs
+#pragma unroll
+    for (int e = 3 * f; e < 3 * f + 3; ++e)
+      wb[e >> 1][e & 1] = *reinterpret_cast<const bf16x8*>(
+          w2 + ((nh * 32 + (e & 1) * 16 + i16) * 9 + (e >> 1)) * 32 + 8 * g);
+  };
+
+  bf16x4 w1f[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
   // 2. conv1 + bias + ReLU -> LDS a1 image; lane holds 4 consecutive channels of one
-  // pixel -> one 8-byte LDS store per 16x16 tile
-  for (int nt = wave; nt < (P1 + 15) / 16; nt += FWD_THREADS / 64) {
-    const int P = min(nt * 16 + i16, P1 - 1);
-    const int y = P / H1, x = P - y * H1;
-    const int xb = y * IMG + x;
-    bf16x4 bx;
+  // pixel -> one 8-byte LDS store per 16x16 tile.  Tiles of 16 "virtual pixels" V = 28y + x
+  // of the 28-wide x image (x = 26, 27 and y >= 26 computed and dropped): V is the pixel's
+  // own x index, x & 3 == lane & 3, so the operand reads are V + a per-lane tap offset and
+  // the a1 store is (V - 2y) * 64 + a per-lane constant.  46 tiles (48 slots) over 8 waves.
+  {
+    constexpr int TPW = 6;
+    int tb[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bx[j] = xs[toff[j] == IMG * IMG ? IMG * IMG : xb + toff[j]];
+    for (int j = 0; j < 4; ++j) tb[j] = toff[j] == IMG * IMG ? 0 : toff[j];   // w = 0 there
+    const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);   // mt = 0; mt = 1: ^ 32
+    // two rounds of 3 tiles: the 72 conv2 B-fragment registers are live here, and 6 tiles'
+    // operands at once would push the kernel past 128 VGPRs (2 workgroups / CU)
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx, b1v[mt], 0, 0, 0);
-      bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
-                  to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
-      if (nt * 16 + i16 < P1)  // channels co = 16mt + 4g .. +3 = byte 32mt + 8g
-        *reinterpret_cast<bf16x4*>(a1s + a1_off(y, x, 32 * mt + 8 * g)) = o;
+    for (int h = 0; h < TPW; h += 3) {
+    bf16x4 bx[TPW];
+    int vv[TPW];
+#pragma unroll
+    for (int k = h; k < h + 3; ++k) {
+      vv[k] = (wave + 8 * k) * 16 + i16;
+      const int vc = min(vv[k], IMG * H1 - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bx[k][j] = xs[vc + tb[j]];
+    }
+#pragma unroll
+    for (int k = h; k < h + 3; ++k) {
+      load_wb(k);
+      const int y = vv[k] / IMG, x = vv[k] - y * IMG;
+      const bool ok = y < H1 && x < H1;
+      const int ab = (vv[k] - 2 * y) * 64 + a1c;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
+        bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
+                    to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
+        if (ok) *reinterpret_cast<bf16x4*>(a1s + (ab ^ (32 * mt))) = o;
+      }
+    }
     }
   }
   __syncthreads();
@@ -182,6 +229,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     uint4* mout = reinterpret_cast<uint4*>(pmask + (int64_t)img * FEAT);
     for (int i = tid; i < FEAT / 16; i += FWD_THREADS) mout[i] = reinterpret_cast<const uint4*>(ms)[i];
   }
+  if (tid == 64) ylab[img] = lab;
   PDM_STAMP(5);
 }
 

@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_cnn_bwd_exact.py tests/test_gpu_cnn.py > gpurun_out/t_cnn.log 2>&1 || exit 1
+: > gpurun_out/kb_fc.log
+for r in all dw dx hr; do
+  PDM_FC1BWD_ROLE=$r timeout -k 10 120 python -u tools/kbench_fc.py 256 >> gpurun_out/kb_fc.log 2>&1 || exit 1
+done
+timeout -k 10 300 python -u tools/kbench.py 256 1024 8192 > gpurun_out/kbench.log 2>&1
+echo rc=$?

@@ -35,43 +35,49 @@ def timeit(fn, iters=50):
     return a.elapsed_time(b) / (3 * iters) * 1e3
 
 
-for B in [int(b) for b in (sys.argv[1:] or ["256", "1024", "4096"])]:
-    p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.01,
-                            use_graphs=False)
-    p.optimizer.sync_hyperparams()
-    p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
-    st = p.gpu
-    C, P, G = st.C, st.P, st.G
-    ldt = -(-B // 32) * 32
-    S = st.splitk_train
-    ipb = choose_ipb(B)
-    st.train_step(B)
-    torch.cuda.synchronize()
-    z = torch.zeros(1, dtype=torch.int64, device="cuda")
-    ks = {
-        "cnn_fwd": lambda: C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, z, B, B,
-                                     P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"],
-                                     st.pool, st.pmask, st.xg, st.ylab),
-        "fc1_fwd": lambda: C.fc1_fwd(st.pool, st.wf1, st.part, B, S),
-        "cnn_head": lambda: C.cnn_head(st.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
-                                       st.ylab, True, st.dh, st.dht, ldt, st.head_slab,
-                                       st.metrics.train_view(), None, None),
-        "fc1_bwd": lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"],
-                                     st.dpool, st.head_slab, G["fc2.weight"], G["fc2.bias"],
-                                     G["fc1.bias"], st.metrics.train_view()),
-        "cnn_bwd": lambda: C.cnn_bwd(st.xg, P["conv1.weight"], P["conv1.bias"], st.dpool, st.pmask,
-                                     st.w2t, B, ipb, st.conv_slab),
-        "conv_reduce": lambda: C.conv_reduce(st.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"],
-                                             G["conv2.bias"], G["conv1.weight"], G["conv1.bias"]),
-        "optim": lambda: st.launch_optimizer(),
-    }
-    tot = 0.0
-    line = []
-    for name, fn in ks.items():
-        us = timeit(fn)
-        tot += us
-        line.append(f"{name}={us:.1f}")
-    st.ctr.zero_()   # each step advances the data counter (rows are clamped past the epoch)
-    step = timeit(lambda: st._train_impl(B), 8)
-    print(f"B={B:5d} S={S} ipb={ipb} " + " ".join(line) + f" | sum={tot:.1f}us step={step:.1f}us "
-          f"-> {B / step * 1e6 / 1e6:.2f}M img/s", flush=True)
+
+def main():
+  for B in [int(b) for b in (sys.argv[1:] or ["256", "1024", "4096"])]:
+      p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.01,
+                              use_graphs=False)
+      p.optimizer.sync_hyperparams()
+      p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+      st = p.gpu
+      C, P, G = st.C, st.P, st.G
+      ldt = -(-B // 32) * 32
+      S = st.splitk_train
+      ipb = choose_ipb(B)
+      st.train_step(B)
+      torch.cuda.synchronize()
+      z = torch.zeros(1, dtype=torch.int64, device="cuda")
+      ks = {
+          "cnn_fwd": lambda: C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, z, B, B,
+                                       P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"],
+                                       st.pool, st.pmask, st.xg, st.ylab),
+          "fc1_fwd": lambda: C.fc1_fwd(st.pool, st.wf1, st.part, B, S),
+          "cnn_head": lambda: C.cnn_head(st.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
+                                         st.ylab, True, st.dh, st.dht, ldt, st.head_slab,
+                                         st.metrics.train_view(), None, None),
+          "fc1_bwd": lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"],
+                                       st.dpool, st.head_slab, G["fc2.weight"], G["fc2.bias"],
+                                       G["fc1.bias"], st.metrics.train_view()),
+          "cnn_bwd": lambda: C.cnn_bwd(st.xg, P["conv1.weight"], P["conv1.bias"], st.dpool, st.pmask,
+                                       st.w2t, B, ipb, st.conv_slab),
+          "conv_reduce": lambda: C.conv_reduce(st.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"],
+                                               G["conv2.bias"], G["conv1.weight"], G["conv1.bias"]),
+          "optim": lambda: st.launch_optimizer(),
+      }
+      tot = 0.0
+      line = []
+      for name, fn in ks.items():
+          us = timeit(fn)
+          tot += us
+          line.append(f"{name}={us:.1f}")
+      st.ctr.zero_()   # each step advances the data counter (rows are clamped past the epoch)
+      step = timeit(lambda: st._train_impl(B), 8)
+      print(f"B={B:5d} S={S} ipb={ipb} " + " ".join(line) + f" | sum={tot:.1f}us step={step:.1f}us "
+            f"-> {B / step * 1e6 / 1e6:.2f}M img/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
