@@ -240,6 +240,12 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
       TORCH_CHECK(sh.numel() == (int64_t)s.rows * s.cols, "shadow_t size mismatch");
       s.shadow_t = ptr<__bf16>(sh);
     }
+    s.tonly = (t.size() > 6 && !t[6].is_none() && t[6].cast<bool>()) ? 1 : 0;
+    if (s.tonly) {
+      TORCH_CHECK(s.shadow != nullptr && s.shadow_t != nullptr && s.slab == nullptr,
+                  "a transpose-only segment needs shadow and shadow_t and no slab");
+      need_aligned(s.shadow, 16, "shadow");
+    }
   }
   a.xg = opt_sync(xg);
   a.xg_signal_ch = (int)signal_ch;
@@ -368,9 +374,54 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
                   train ? xg_step(xg) : nullptr, cur_stream(part));
 }
 
+// fc_update (world size 1, optional): (kind, p, g, m, v or None, shadow, lr, step, beta1,
+// beta2, eps, wd, momentum, dampening, nesterov, grad_scale) -- the fc1-weight update of the
+// optimizer, run by cnn_bwd (kernels.h FcUpdate)
+static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
+  FcUpdate u{};
+  u.kind = -1;
+  if (!t.has_value()) return u;
+  const py::tuple& a = *t;
+  TORCH_CHECK(a.size() == 16, "fc_update: 16 entries");
+  u.kind = (int)a[0].cast<int64_t>();
+  TORCH_CHECK(u.kind == OPT_SGD, "fc_update: SGD-momentum only (Adam runs in the optimizer kernel)");
+  auto p = a[1].cast<at::Tensor>(), g = a[2].cast<at::Tensor>(), m = a[3].cast<at::Tensor>();
+  auto sh = a[5].cast<at::Tensor>(), lr = a[6].cast<at::Tensor>(), st = a[7].cast<at::Tensor>();
+  need(p, at::kFloat, "fc p");
+  need(g, at::kFloat, "fc g");
+  need(m, at::kFloat, "fc m");
+  need(sh, at::kBFloat16, "fc shadow");
+  need(lr, at::kDouble, "lr");
+  need(st, at::kLong, "step");
+  u.numel = p.numel();
+  TORCH_CHECK(u.numel == (int64_t)CNN_HID * CNN_FEAT && g.numel() == u.numel &&
+                  m.numel() == u.numel && sh.numel() == u.numel, "fc_update: fc1 weight sizes");
+  for (const void* q : {p.data_ptr(), g.data_ptr(), m.data_ptr()}) need_aligned(q, 16, "fc_update fp32");
+  need_aligned(sh.data_ptr(), 8, "fc_update shadow");
+  u.p = p.data_ptr<float>();
+  u.g = g.data_ptr<float>();
+  u.m = m.data_ptr<float>();
+  u.v = nullptr;
+  u.shadow = ptr<__bf16>(sh);
+  u.lr = lr.data_ptr<double>();
+  u.step = st.data_ptr<int64_t>();
+  u.beta1_d = a[8].cast<double>();
+  u.beta2_d = a[9].cast<double>();
+  u.beta1 = (float)u.beta1_d;
+  u.beta2 = (float)u.beta2_d;
+  u.eps = (float)a[10].cast<double>();
+  u.wd = (float)a[11].cast<double>();
+  u.momentum = (float)a[12].cast<double>();
+  u.dampening = (float)a[13].cast<double>();
+  u.nesterov = a[14].cast<bool>() ? 1 : 0;
+  u.grad_scale = (float)a[15].cast<double>();
+  return u;
+}
+
 void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Tensor wf1t,
              int64_t B, at::Tensor gwf1, at::Tensor dpool, at::Tensor head_slab, at::Tensor gwf2,
-             at::Tensor gbf2, at::Tensor gbf1, at::Tensor metrics) {
+             at::Tensor gbf2, at::Tensor gbf1, at::Tensor metrics,
+             c10::optional<py::tuple> fc_update) {
   c10::DeviceGuard g(dh.device());
   TORCH_CHECK(B >= 1 && ldt % 32 == 0 && ldt >= B, "bad ldt/B");
   need_min(dh, at::kBFloat16, ldt * CNN_HID, "dh");
@@ -391,7 +442,7 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
   launch_fc1_bwd(ptr<__bf16>(dh), ptr<__bf16>(dht), (int)ldt, ptr<__bf16>(pool), ptr<__bf16>(wf1t),
                  (int)B, gwf1.data_ptr<float>(), ptr<__bf16>(dpool), head_slab.data_ptr<float>(),
                  (int)hb, gwf2.data_ptr<float>(), gbf2.data_ptr<float>(), gbf1.data_ptr<float>(),
-                 metrics.data_ptr<double>(), cur_stream(dh));
+                 metrics.data_ptr<double>(), make_fc_update(fc_update), cur_stream(dh));
 }
 
 void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::Tensor pmask,
@@ -486,7 +537,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
         py::arg("dht"), py::arg("ldt"), py::arg("slab"), py::arg("metrics"), py::arg("c0"),
         py::arg("c1"), py::arg("xg") = py::none());
-  m.def("fc1_bwd", &fc1_bwd);
+  m.def("fc1_bwd", &fc1_bwd, py::arg("dh"), py::arg("dht"), py::arg("ldt"), py::arg("pool"),
+        py::arg("wf1t"), py::arg("B"), py::arg("gwf1"), py::arg("dpool"), py::arg("head_slab"),
+        py::arg("gwf2"), py::arg("gbf2"), py::arg("gbf1"), py::arg("metrics"),
+        py::arg("fc_update") = py::none());
   m.def("cnn_bwd", &cnn_bwd, py::arg("xg"), py::arg("w1"), py::arg("b1"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2t"), py::arg("B"), py::arg("ipb"), py::arg("slab"),
         py::arg("xg_sync") = py::none());

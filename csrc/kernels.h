@@ -43,6 +43,9 @@ struct OptSeg {
   // optional (xgmi streamed mode): wait until DONE[wait_ch] >= wait_mult * STEP
   int32_t wait_ch;
   uint32_t wait_mult;
+  // transpose-only segment: no update; shadow_t is re-derived from shadow (the update ran
+  // elsewhere, e.g. fused into cnn_bwd at world size 1)
+  int32_t tonly;
 };
 
 struct OptArgs {
@@ -66,6 +69,27 @@ struct OptArgs {
 };
 
 void launch_optim(int kind, OptArgs& a, hipStream_t st);
+
+// World size 1: the fc1-weight update fused into fc1_bwd's weight-gradient tiles (the tile
+// is final in registers; nothing else in the step reads the fp32 weights or the bf16 [n][k]
+// copy until the next step's fc1_fwd -- the transposed copy that this step's dX tiles read
+// is re-derived later by the optimizer launch).  kind < 0: off; OPT_SGD only.  Same
+// hyper-parameter fields as OptArgs.
+struct FcUpdate {
+  int kind;
+  int64_t numel;        // multiple of 4
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  __bf16* shadow;       // bf16 copy, same layout
+  const double* lr;
+  const int64_t* step;
+  double beta1_d, beta2_d;
+  float beta1, beta2, eps, wd, momentum, dampening;
+  int nesterov;
+  float grad_scale;
+};
 
 // ---------------------------------------------------------------- CNN (bf16)
 // Layouts (NHWC, see pytorch_distributed_mnist_amd/models/specs.py):
@@ -102,7 +126,7 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
-                    hipStream_t st);
+                    const FcUpdate& fcu, hipStream_t st);
 void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
                     const uint8_t* pmask, const __bf16* w2t, int B, int imgs_per_block, float* slab,
                     unsigned* xg_sync, hipStream_t st);

@@ -20,6 +20,7 @@
 //                and writes one fp32 slab per block (no atomics, deterministic).
 //   conv_reduce: fixed-order slab sum -> conv gradients (bucket 1 complete).
 #include "cnn_common.h"
+#include "optim_common.h"
 #include "xgmi.h"
 
 #include <cstdlib>
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const bf16* __restrict__ pool, const bf16* __restrict__ wf1t, int B, float* __restrict__ gwf1,
     bf16* __restrict__ dpool, const float* __restrict__ head_slab, int head_blocks,
     float* __restrict__ gwf2, float* __restrict__ gbf2, float* __restrict__ gbf1,
-    double* __restrict__ metrics, int bid_offset) {
+    double* __restrict__ metrics, int bid_offset, const FcUpdate fcu) {
   __shared__ __attribute__((aligned(16))) char tile[DWC * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
@@ -98,6 +99,21 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
               dht + (int64_t)(wave * 32 + mt * 16 + i16) * ldt + min(c0 + 32 * kk, ldt - 32) + 8 * g);
     };
     load_chunk(0);
+    // fused update (fcu.kind >= 0): this tile's fp32 weights and momentum, issued behind the
+    // first chunk so they have landed by the epilogue
+    float fpv[2][4][4], fmv[2][4][4];
+    if (fcu.kind >= 0) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int64_t q = (int64_t)(wave * 32 + mt * 16 + 4 * g + r) * FEAT + k0 + 16 * nt + i16;
+            fpv[mt][r][nt] = fcu.p[q];
+            fmv[mt][r][nt] = fcu.m[q];
+          }
+    }
     for (int c0 = 0; c0 < ldt; c0 += DWC) {
       __syncthreads();   // previous chunk's tile reads are done
 #pragma unroll
@@ -135,6 +151,27 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + 16 * nt + i16] = acc[mt][nt][r];
       }
+    if (fcu.kind >= 0) {
+      // world size 1 (kernels.h FcUpdate): the SGD-momentum update of this tile, from the
+      // gradient still in registers; writes the fp32 weight, the momentum and the bf16 [n][k]
+      // copy (the transposed copy, which this launch's dX tiles are reading, is re-derived
+      // by the optimizer launch).  Same op order as the optimizer kernel: same bits.
+      using namespace optim_detail;
+      const Hyper h = make_hyper<OPT_SGD>(fcu);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int64_t q = (int64_t)(wave * 32 + mt * 16 + 4 * g + r) * FEAT + k0 + 16 * nt + i16;
+            float m = fmv[mt][r][nt], v = 0.f;
+            const float p = update<OPT_SGD>(fpv[mt][r][nt], acc[mt][nt][r], m, v, h, fcu.grad_scale);
+            fcu.p[q] = p;
+            fcu.m[q] = m;
+            fcu.shadow[q] = to_bf16(p);
+          }
+    }
     return;
   }
 
@@ -852,7 +889,7 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
-                    hipStream_t st) {
+                    const FcUpdate& fcu, hipStream_t st) {
   const int nd = (ldt / 32) * DX_TILES;
   int nblk = DW_TILES + nd + HR_BLOCKS, off = 0;
   // diagnostic only (tools/kbench.py): PDM_FC1BWD_ROLE=dw|dx|hr launches one role alone
@@ -861,7 +898,7 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
   else if (role && role[0] == 'd' && role[1] == 'x') { nblk = nd; off = DW_TILES; }
   else if (role && role[0] == 'h') { nblk = HR_BLOCKS; off = DW_TILES + nd; }
   fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, dht, ldt, pool, wf1t, B, gwf1, dpool, head_slab,
-                                       head_blocks, gwf2, gbf2, gbf1, metrics, off);
+                                       head_blocks, gwf2, gbf2, gbf1, metrics, off, fcu);
 }
 
 int cnn_bwd_blocks(int B, int ipb) { return (B + ipb - 1) / ipb; }

@@ -15,64 +15,15 @@
 //     the transposed bf16 store stay coalesced.
 #include "common.h"
 #include "kernels.h"
+#include "optim_common.h"
 #include "xgmi.h"
 
 namespace {
 
+using namespace optim_detail;
+
 constexpr int CHUNK = 2048;  // elements per block for plain segments (256 thr x 8)
 constexpr int TR = 32, TC = 64;
-
-struct Hyper {
-  float lr, step_size, bc2_sqrt, beta1, beta2, eps, wd, mom, damp;
-  int first, nesterov;
-};
-
-template <int KIND>
-__device__ __forceinline__ Hyper make_hyper(const OptArgs& a) {
-  Hyper h;
-  const double lr = *a.lr;
-  const int64_t t = *a.step;
-  h.lr = (float)lr;
-  h.beta1 = a.beta1; h.beta2 = a.beta2; h.eps = a.eps; h.wd = a.wd;
-  h.mom = a.momentum; h.damp = a.dampening; h.nesterov = a.nesterov;
-  h.first = (t <= 1);
-  if (KIND == OPT_ADAM) {
-    // torch: bias_correction1 = 1 - beta1 ** step (python double), step_size = lr / bc1,
-    //        bias_correction2_sqrt = (1 - beta2 ** step) ** 0.5
-    const double bc1 = 1.0 - pow((double)a.beta1_d, (double)t);
-    const double bc2 = 1.0 - pow((double)a.beta2_d, (double)t);
-    h.step_size = (float)(lr / bc1);
-    h.bc2_sqrt = (float)sqrt(bc2);
-  } else {
-    h.step_size = 0.f;
-    h.bc2_sqrt = 1.f;
-  }
-  return h;
-}
-
-template <int KIND>
-__device__ __forceinline__ float update(float p, float g, float& m, float& v, const Hyper& h,
-                                        float gs) {
-  // torch rounds after every op (mul_, add_, addcmul_, ...): no FMA contraction, which
-  // also keeps every code path of this kernel bit-identical
-#pragma clang fp contract(off)
-  g *= gs;
-  if (h.wd != 0.f) g = fmaf(h.wd, p, g);  // grad.add(param, alpha=wd)
-  if (KIND == OPT_ADAM) {
-    const float w = 1.f - h.beta1;  // exp_avg.lerp_(grad, 1 - beta1)
-    m = (w < 0.5f) ? m + w * (g - m) : g - (g - m) * (1.f - w);
-    v = v * h.beta2 + (1.f - h.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1 - beta2)
-    const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
-    return p + (-h.step_size) * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
-  } else {
-    float d = g;
-    if (h.mom != 0.f) {
-      m = h.first ? d : m * h.mom + (1.f - h.damp) * d;
-      d = h.nesterov ? d + h.mom * m : m;
-    }
-    return p + (-h.lr) * d;
-  }
-}
 
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
@@ -93,6 +44,36 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     }
     __syncthreads();
     if (!s_go) return;     // a peer never arrived: error bit set, the host raises
+  }
+  if (s.tonly) {
+    // transpose-only: shadow_t = shadow^T for a TR x TC tile (bf16 in, bf16 out)
+    __shared__ __attribute__((aligned(16))) bf16 tt[TC][TR + 8];
+    const int tiles_c = (s.cols + TC - 1) / TC;
+    const int tr0 = (lb / tiles_c) * TR, tc0 = (lb % tiles_c) * TC;
+    const int r = threadIdx.x >> 3, c8 = (threadIdx.x & 7) * 8;
+    const int row = tr0 + r, col0 = tc0 + c8;
+    if (row < s.rows && col0 < s.cols) {
+      const int64_t e = (int64_t)row * s.cols + col0;
+      if (col0 + 8 <= s.cols && (e & 7) == 0) {
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(s.shadow + e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tt[c8 + j][r] = hb[j];
+      } else {
+        for (int j = 0; j < 8 && col0 + j < s.cols; ++j) tt[c8 + j][r] = s.shadow[e + j];
+      }
+    }
+    __syncthreads();
+    const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 8;
+    const int col = tc0 + c;
+    if (col < s.cols) {
+      const int64_t base = (int64_t)col * s.rows + tr0 + rr;
+      if (tr0 + rr + 8 <= s.rows && (base & 7) == 0) {
+        *reinterpret_cast<bf16x8*>(s.shadow_t + base) = *reinterpret_cast<const bf16x8*>(&tt[c][rr]);
+      } else {
+        for (int j = 0; j < 8 && tr0 + rr + j < s.rows; ++j) s.shadow_t[base + j] = tt[c][rr + j];
+      }
+    }
+    return;
   }
   const Hyper h = make_hyper<KIND>(a);
   float* __restrict__ P = a.p + s.offset;
@@ -262,7 +243,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
 
 int opt_blocks_for(const OptSeg& s) {
   if (s.slab) return (int)(((int64_t)s.rows * s.cols + 63) / 64);
-  if (s.shadow_t) return ((s.rows + TR - 1) / TR) * ((s.cols + TC - 1) / TC);
+  if (s.shadow_t || s.tonly) return ((s.rows + TR - 1) / TR) * ((s.cols + TC - 1) / TC);
   const int64_t n = (int64_t)s.rows * s.cols;
   return (int)((n + CHUNK - 1) / CHUNK);
 }

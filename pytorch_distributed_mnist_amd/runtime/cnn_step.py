@@ -89,6 +89,12 @@ class CnnStep(GpuStepBase):
         # reduction is fused into the optimizer launch (PDM_FUSE_CONV_REDUCE=0 disables)
         self.fuse_conv_reduce = (not self.reducer.active and
                                  os.environ.get("PDM_FUSE_CONV_REDUCE", "1") != "0")
+        # world_size 1, SGD-momentum: the fc1-weight update runs in fc1_bwd's weight-gradient
+        # tiles (the gradient is still in registers; those tiles have slack next to the dX
+        # tiles of the same launch); the optimizer launch then only re-derives the transposed
+        # bf16 copy W1^T from the updated W1 (PDM_FUSE_FC1=0 disables)
+        self.fuse_fc1 = (self.fuse_conv_reduce and self.opt.kind == "sgd" and
+                         os.environ.get("PDM_FUSE_FC1", "1") != "0")
         self._fused = {}
         self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
         self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
@@ -155,9 +161,13 @@ class CnnStep(GpuStepBase):
                    "conv1.weight": C.CNN_CONV_SLAB_DW1, "conv1.bias": C.CNN_CONV_SLAB_DB1}
             by_off = {self.arena.spec.offset(n): n for n in col}
             slab_segs, plain = [], []
+            fc1_off = self.arena.spec.offset("fc1.weight")
             for sg in self._opt_segments:
                 name = by_off.get(sg[0])
-                if name is None:
+                if name is None and self.fuse_fc1 and sg[0] == fc1_off:
+                    # updated by cnn_bwd: only W1^T = transpose(W1) is left to write
+                    plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True))
+                elif name is None:
                     plain.append(sg)
                 else:
                     slab_segs.append(tuple(sg) +
@@ -205,7 +215,8 @@ class CnnStep(GpuStepBase):
                    self.ctr[0:1], self.opt._step_dev, xs)
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
-                  self.metrics.train_view())
+                  self.metrics.train_view(),
+                  self._fc_update() if self.fuse_fc1 and self.fuse_conv_reduce else None)
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
         early = xgmi and not red.streamed and os.environ.get("PDM_XGMI_EARLY", "1") != "0"
         if early:
@@ -259,6 +270,17 @@ class CnnStep(GpuStepBase):
         if not carry_out:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(b0)
+
+    def _fc_update(self):
+        """fc1_bwd's fused fc1-weight SGD update (bind.cpp make_fc_update)."""
+        o = self.opt
+        g = o.param_groups[0]
+        off = self.arena.spec.offset("fc1.weight")
+        n = 128 * 9216
+        return (self.C.OPT_SGD, self.arena.params[off:off + n], self.reducer.out_grads[off:off + n],
+                o.momentum_buffer[off:off + n], None, self.wf1, o._lr_dev, o._step_dev, 0.0, 0.0,
+                0.0, float(g["weight_decay"]), float(g["momentum"]), float(g["dampening"]),
+                bool(g["nesterov"]), float(self.reducer.grad_scale))
 
     def evaluate(self) -> None:
         C, P = self.C, self.P

@@ -170,17 +170,22 @@ def test_cnn_large_batch_steps(gpu):
 
 
 def test_fused_conv_reduce_matches_separate_pass(gpu):
-    """world_size 1 folds the conv slab reduction into the optimizer launch; it must give the
-    same bits as conv_reduce + optimizer (same fixed summation order), incl. a tail step."""
+    """world_size 1 folds the conv slab reduction into the optimizer launch and (SGD) the
+    fc1-weight update into cnn_bwd; every combination must give the same bits as
+    conv_reduce + optimizer (same fixed summation order, same update op order), incl. a
+    tail step and the bf16 weight copies the next step reads."""
     res = []
-    for fuse in (True, False):
+    for fuse, fuse_fc1 in ((True, True), (True, False), (False, False)):
         prog, train, _ = _program(96, lr=0.05, n=96 * 3 + 40, seed=5)
         prog.gpu.fuse_conv_reduce = fuse
+        prog.gpu.fuse_fc1 = fuse_fc1
         prog.gpu.invalidate_graphs()
         prog.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         prog.train_epoch()
         torch.cuda.synchronize()
         res.append((prog.arena.params.clone(), prog.arena.grads.clone(),
-                    prog.optimizer.momentum_buffer.clone()))
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)
+                    prog.optimizer.momentum_buffer.clone(), prog.gpu.wf1.clone(),
+                    prog.gpu.wf1t.clone()))
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert torch.equal(a, b)

@@ -60,12 +60,15 @@ def main():
                                          st.metrics.train_view(), None, None),
           "fc1_bwd": lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"],
                                        st.dpool, st.head_slab, G["fc2.weight"], G["fc2.bias"],
-                                       G["fc1.bias"], st.metrics.train_view()),
+                                       G["fc1.bias"], st.metrics.train_view(),
+                                       st._fc_update() if st.fuse_fc1 else None),
           "cnn_bwd": lambda: C.cnn_bwd(st.xg, P["conv1.weight"], P["conv1.bias"], st.dpool, st.pmask,
                                        st.w2t, B, ipb, st.conv_slab),
           "conv_reduce": lambda: C.conv_reduce(st.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"],
                                                G["conv2.bias"], G["conv1.weight"], G["conv1.bias"]),
-          "optim": lambda: st.launch_optimizer(),
+          # the training step's update: the slab-fused launch at world size 1
+          "optim": (lambda: st.launch_optimizer(st._fused_segments(C.cnn_bwd_nblk(B, ipb))))
+                   if st.fuse_conv_reduce else (lambda: st.launch_optimizer()),
       }
       tot = 0.0
       line = []
