@@ -622,6 +622,9 @@ static_assert(DG_MTP == 4, "dgrad passes: 3 x 4 tiles per wave (the wgrad waves 
               "a workgroup has one image)");
 static_assert(DG_PFD * (DG_MTP + 2) <= 15, "in-flight LDS reads must fit lgkmcnt");
 
+// ONE: one image per workgroup (B <= CUs).  Its own kernel, so that register allocation of the
+// straight-line single-image code is not shaped by the multi-image loop (and vice versa).
+template <bool ONE>
 __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     const uint8_t* __restrict__ xg, const float* __restrict__ w1, const float* __restrict__ b1,
     const bf16* __restrict__ dpool, const uint8_t* __restrict__ pmask,
@@ -651,15 +654,6 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     // ks takes chunk 4ks+g; its lane q reads pixels x = col0+q and x+4 (col0 % 8 == 0).
     f32x4 acc[5][4];   // zeroed after the first image's staging (not live through it)
     const bool five = wave < 2;  // 18 pairs over 4 waves: 5,5,4,4 (+1 discarded on 2,3)
-    int cpair[5];
-#pragma unroll
-    for (int pi = 0; pi < 5; ++pi) {
-      const int pair = min(wave + 4 * pi, 17);
-      const int tap = pair >> 1, nt = pair & 1;
-      const int ky = tap / 3, kx = tap - 3 * ky;
-      cpair[pi] = (ky * H1 + kx) * 64 + (((2 * nt + (pq >> 1)) ^ ((q + kx) & 3)) << 4) + 8 * (pq & 1);
-    }
-    const int u8b = 8 * (pq & 1);
     // Operand addresses of k-step ks = 3m + j: lane group g reads dz2/a1 row 4m + r_j,
     // columns 8c_j + q (and + 4), with 4j + g = 3r_j + c_j.  The dz2 rotation (4 row + x)
     // mod 8 does not depend on m, so every address is a per-lane base of (j, fragment) plus
@@ -668,10 +662,23 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     // (filled after the first image's loads are issued: 51 VALU-computed registers that
     // would otherwise delay the wgrad waves' share of the staging loads)
     auto setup_addr = [&]() __attribute__((always_inline)) {
+    // recomputed per image from a laundered lane id: hoisted out of the image loop, these
+    // addresses (or their lane-dependent parts) would stay live through the staging and spill
+    int ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const int g = ln >> 4, q = (ln >> 2) & 3, pq = ln & 3;
+    int cp[5];
+#pragma unroll
+    for (int pi = 0; pi < 5; ++pi) {
+      const int pair = min(wave + 4 * pi, 17);
+      const int tap = pair >> 1, nt = pair & 1;
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      cp[pi] = (ky * H1 + kx) * 64 + (((2 * nt + (pq >> 1)) ^ ((q + kx) & 3)) << 4) + 8 * (pq & 1);
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int v = 4 * j + g, rj = v / 3, xj = (v - 3 * rj) * 8 + q;
-      const int dbase = B_DZ + (rj * DS + xj) * 128 + u8b;
+      const int dbase = B_DZ + (rj * DS + xj) * 128 + 8 * (pq & 1);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         // chunk 2mt + (pq >> 1) rotated by (4 row + x); pixel x + 4 is rotated 4 further,
@@ -681,7 +688,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
         abA2[j][mt] = dbase + 512 + (co ^ 64);
       }
 #pragma unroll
-      for (int pi = 0; pi < 5; ++pi) abB[j][pi] = B_A1 + (rj * H1 + xj) * 64 + cpair[pi];
+      for (int pi = 0; pi < 5; ++pi) abB[j][pi] = B_A1 + (rj * H1 + xj) * 64 + cp[pi];
     }
     };
     auto rd_a = [&](int ks, int mt) __attribute__((always_inline)) {
@@ -728,10 +735,10 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
     // the accumulators persist across the workgroup's images; after the last image they
     // are stored while the dgrad waves are still computing.  dW2[co][tap][ci]: rows
     // co = 16mt + 4g + r, col ci = 16nt + i16
-    auto per_image = [&](auto first, int i, bool last) __attribute__((always_inline)) {
+    auto per_image = [&](auto first, auto one, int i, bool last) __attribute__((always_inline)) {
       const int img = blockIdx.x * ipb + i;
       if (img < B) bwd_load_image<decltype(first)::value>(smem, img, xg, dpool, pmask, w1, b1, w2t, db2p);
-      if constexpr (decltype(first)::value) setup_addr();
+      setup_addr();
       __syncthreads();
       if constexpr (decltype(first)::value) {
 #pragma unroll
@@ -748,27 +755,34 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           if (pi == 4 && !five) break;
           const int pair = wave + 4 * pi;
           const int tap = pair >> 1, nt = pair & 1;
+          int o;   // laundered: 20 hoisted 64-bit store addresses would be spilled
+          asm volatile("v_mov_b32 %0, %1" : "=v"(o) : "v"(4 * g * 288 + i16));
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + nt * 16 + i16] = acc[pi][mt][r];
+              out[o + (mt * 16 + r) * 288 + tap * 32 + nt * 16] = acc[pi][mt][r];
         }
         PDM_STAMP(3);
       }
       // one image per workgroup: with its accumulators stored, this wave also takes the
       // last dgrad pass (tiles 32 + wave + 4k), which balances the two wave groups (the
       // wgrad's 360 MFMAs vs the dgrad's 432 + epilogues)
-      if constexpr (decltype(first)::value) {
-        if (ipb == 1 && img < B && PDM_ABL != 2)
+      if constexpr (decltype(one)::value) {
+        if (img < B && PDM_ABL != 2)
           dgrad_pass<DG_MTP, DG_PFD>(smem, 32 + wave, ka1, acc1, t_mf, t_ep);
       }
       __syncthreads();
     };
-    // one image per workgroup (B <= CUs): straight-line code, nothing hoisted out of an
-    // image loop (hipcc would keep the loop-invariant addresses live and spill)
-    per_image(std::true_type{}, 0, ipb == 1);
-    for (int i = 1; i < ipb; ++i) per_image(std::false_type{}, i, i == ipb - 1);
+    // one image per workgroup (B <= CUs) is its own straight-line instantiation: there the
+    // wgrad accumulators are dead once stored, so they are not live (and spilled) through
+    // the dgrad pass the same waves run next
+    if constexpr (ONE) {
+      per_image(std::true_type{}, std::true_type{}, 0, true);
+    } else {
+      per_image(std::true_type{}, std::false_type{}, 0, false);
+      for (int i = 1; i < ipb; ++i) per_image(std::false_type{}, std::false_type{}, i, i == ipb - 1);
+    }
   } else {
     // ===== conv2 input gradient + relu'(a1) + conv1 weight/bias gradient =====
     const int wd = wave - 4;
@@ -780,7 +794,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
         // tiles wd + 4j, j < 12, in passes of DG_MTP tiles; a rolled pass loop keeps one
         // copy of the pass code and stops cross-pass scheduling
         // (one image per workgroup: the wgrad waves take the last pass)
-        const int npass = ipb == 1 ? 12 / DG_MTP - 1 : 12 / DG_MTP;
+        const int npass = ONE ? 12 / DG_MTP - 1 : 12 / DG_MTP;
 #pragma unroll 1
         for (int ps = 0; ps < npass; ++ps)
           dgrad_pass<DG_MTP, DG_PFD>(smem, wd + 4 * DG_MTP * ps, ka1, acc1, t_mf, t_ep);
@@ -788,7 +802,8 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
       __syncthreads();
     };
     per_image(std::true_type{}, 0);
-    for (int i = 1; i < ipb; ++i) per_image(std::false_type{}, i);
+    if constexpr (!ONE)
+      for (int i = 1; i < ipb; ++i) per_image(std::false_type{}, i);
     if (tid == 256) {
       PDM_STAMP_VAL(8, t_mf);
       PDM_STAMP_VAL(9, t_ep);
@@ -906,8 +921,12 @@ int cnn_bwd_blocks(int B, int ipb) { return (B + ipb - 1) / ipb; }
 void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
                     const uint8_t* pmask, const __bf16* w2t, int B, int ipb, float* slab,
                     unsigned* xg_sync, hipStream_t st) {
-  cnn_bwd_kernel<<<cnn_bwd_blocks(B, ipb), BWD_THREADS, 0, st>>>(xg, w1, b1, dpool, pmask, w2t, B,
-                                                                 ipb, slab, xg_sync);
+  if (ipb == 1)
+    cnn_bwd_kernel<true><<<cnn_bwd_blocks(B, ipb), BWD_THREADS, 0, st>>>(xg, w1, b1, dpool, pmask,
+                                                                       w2t, B, ipb, slab, xg_sync);
+  else
+    cnn_bwd_kernel<false><<<cnn_bwd_blocks(B, ipb), BWD_THREADS, 0, st>>>(xg, w1, b1, dpool, pmask,
+                                                                        w2t, B, ipb, slab, xg_sync);
 }
 
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
