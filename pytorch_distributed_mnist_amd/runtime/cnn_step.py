@@ -165,7 +165,7 @@ class CnnStep(GpuStepBase):
             for sg in self._opt_segments:
                 name = by_off.get(sg[0])
                 if name is None and self.fuse_fc1 and sg[0] == fc1_off:
-                    # updated by cnn_bwd: only W1^T = transpose(W1) is left to write
+                    # updated by fc1_bwd: only W1^T = transpose(W1) is left to write
                     plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True))
                 elif name is None:
                     plain.append(sg)

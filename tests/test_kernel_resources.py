@@ -1,0 +1,61 @@
+"""Resource budget of the built gfx950 kernels (CPU-only: reads the code-object metadata).
+
+A scratch spill inside a hot loop costs a memory round trip per use, and hipcc spills
+silently (round 2 found 180 B of scratch in cnn_bwd's multi-image path), so every kernel
+is pinned to zero scratch.  The LDS / register budgets pin the occupancy each kernel's
+design assumes (docs/kernels.md).
+"""
+import glob
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = sorted(glob.glob(os.path.join(ROOT, "pytorch_distributed_mnist_amd", "_C*.so")))
+
+pytestmark = pytest.mark.skipif(
+    not SO or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"),
+    reason="extension not built or ROCm llvm tools absent")
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_resources import kernels as read
+    ks = read(SO[0])
+    assert ks, "no kernels found in the extension's code objects"
+    return ks
+
+
+def _find(ks, name):
+    hits = {k: v for k, v in ks.items() if name in k}
+    assert hits, f"kernel {name} not found"
+    return hits
+
+
+def test_no_kernel_uses_scratch(kernels):
+    spilled = {k: v["private_segment_fixed_size"] for k, v in kernels.items()
+               if v.get("private_segment_fixed_size", 0) != 0}
+    assert not spilled, f"kernels with scratch: {spilled}"
+
+
+def test_every_hot_kernel_is_present(kernels):
+    for name in ("cnn_fwd_kernel", "fc1_fwd_kernel", "cnn_head_kernel", "fc1_bwd_kernel",
+                 "cnn_bwd_kernel", "conv_reduce_kernel", "optim_kernel", "lin_train_kernel",
+                 "xgmi_allreduce_kernel"):
+        _find(kernels, name)
+
+
+def test_occupancy_budgets(kernels):
+    # cnn_bwd: one 512-thread workgroup per CU (its LDS carve), <= 256 registers per lane
+    for k, v in _find(kernels, "cnn_bwd_kernel").items():
+        assert v["group_segment_fixed_size"] <= 163840, k
+        assert v["vgpr_count"] + v.get("agpr_count", 0) <= 256, k
+    # cnn_fwd: two 512-thread workgroups per CU (<= 80 KB LDS, <= 128 registers)
+    for k, v in _find(kernels, "cnn_fwd_kernel").items():
+        assert v["group_segment_fixed_size"] <= 81920, k
+        assert v["vgpr_count"] + v.get("agpr_count", 0) <= 128, k
+    # fc1_bwd: 256 threads, one wave per SIMD per workgroup, all roles one round
+    for k, v in _find(kernels, "fc1_bwd_kernel").items():
+        assert v["vgpr_count"] + v.get("agpr_count", 0) <= 512, k
