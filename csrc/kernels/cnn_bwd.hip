@@ -445,7 +445,10 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   // builds the 16-B chunk of each of the window's 4 pixels (the pooled gradient at the
   // channel's argmax position if it was > 0, zero elsewhere) and stores 4 x 16 B.
   // For window pos s = 2dy + dx the pixel is (2py + dy, 2px + dx), rotation 4(2py + dy) +
-  // 2px + dx.
+  // 2px + dx.  Mask byte (cnn_fwd): 0x80 | 1 << s if the pooled value is > 0, else 0.
+  // VALU-lean (this phase is VALU-bound: 8 waves, 2 per SIMD): the keep-mask of a bf16 pair
+  // is one v_perm_b32 that replicates two flag bits, moved to bits 15 / 31 of its sources by
+  // one shift each, into the two halves of the word.
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int it = tid + k * BWD_THREADS;   // it & 7 == tid & 7: fixed channel chunk
@@ -456,23 +459,28 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
       const int b0 = 2 * px + ch;                 // + 4 (2py + dy) + dx: 8py drops mod 8
       const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
       const uint32_t mw[2] = {mk[k].x, mk[k].y};
-      uint32_t sel[8];                       // per channel: window position, or 4 if <= 0
+      // conv2 bias gradient: the pooled gradients of positive pooled values
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t mb = (mw[j >> 2] >> (8 * (j & 3))) & 0xff;
-        const uint32_t dv = (dw[j >> 1] >> (16 * (j & 1))) & 0xffff;
-        sel[j] = (mb & 0x80) ? (mb & 3) : 4u;
-        db2p[j] += __builtin_bit_cast(float, ((mb & 0x80) ? dv : 0u) << 16);
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t sh = mw[h] << 8;           // bit 15 / 31: flag of channel 4h / 4h + 2
+        const uint32_t pos[2] = {__builtin_amdgcn_perm(mw[h], sh, 0x0A0A0808u),
+                                 __builtin_amdgcn_perm(mw[h], sh, 0x0B0B0909u)};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t w = dw[2 * h + e] & pos[e];
+          db2p[4 * h + 2 * e] += __builtin_bit_cast(float, w << 16);
+          db2p[4 * h + 2 * e + 1] += __builtin_bit_cast(float, w & 0xffff0000u);
+        }
       }
 #pragma unroll
       for (int sw = 0; sw < 4; ++sw) {
         uint4 o;
         uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t w = dw[q];
-          ow[q] = (sel[2 * q] == (uint32_t)sw ? (w & 0xffffu) : 0u) |
-                  (sel[2 * q + 1] == (uint32_t)sw ? (w & 0xffff0000u) : 0u);
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t u = mw[h] << (7 - sw), v = mw[h] << (15 - sw);
+          ow[2 * h] = dw[2 * h] & __builtin_amdgcn_perm(u, v, 0x0A0A0808u);
+          ow[2 * h + 1] = dw[2 * h + 1] & __builtin_amdgcn_perm(u, v, 0x0B0B0909u);
         }
         const int off = base + (sw >> 1) * (DS * 128) + (sw & 1) * 128 +
                         (((b0 + 4 * (sw >> 1) + (sw & 1)) & 7) << 4);

@@ -7,7 +7,8 @@
 //             input channels), with bias + ReLU + MaxPool2d(2) fused in-register:
 //             the M rows of a 16-row tile are ordered (pooled pixel, window pos), so a
 //             lane's 4 accumulator registers ARE one 2x2 window.  Writes the pooled
-//             activations (fc1 input), a 1-byte argmax|positive mask per pooled value,
+//             activations (fc1 input), a 1-byte mask per pooled value (0x80 | 1 << argmax
+//             if positive, else 0),
 //             and (training) a1 + the gathered bytes for the backward kernel.
 //   fc1_fwd : split-K bf16 GEMM  part[s] = pool[:, Ks] . W1[:, Ks]^T  (fp32 slabs),
 //             the reduction + bias + ReLU is fused into the head kernel.
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
         if (v > best) { best = v; bi = r; }          // first max in (dy, dx) row-major order
       }
       ps[pp * C2 + co] = to_bf16(best);
-      ms[pp * C2 + co] = (uint8_t)(bi | (best > 0.f ? 0x80 : 0));
+      ms[pp * C2 + co] = (uint8_t)(best > 0.f ? 0x80 | (1 << bi) : 0);   // one-hot argmax
     }
   }
   PDM_STAMP(3);

@@ -73,7 +73,10 @@ def test_cnn_forward_kernels(gpu, B):
     top2 = win.topk(2, dim=-1).values
     clear = (top2[..., 0] - top2[..., 1]) > 1e-2
     ref_s = (arg // 24 % 2) * 2 + (arg % 24 % 2)
-    assert ((mask & 3) == ref_s)[clear & pos].all()
+    # one-hot argmax (0x80 | 1 << s) on positive values, 0 elsewhere
+    assert (mask[~pos] == 0).all()
+    assert ((mask & 0x0F) == (1 << ref_s))[clear & pos].all()
+    assert (((mask & 0x0F) & ((mask & 0x0F) - 1)) == 0).all()   # one bit at most
 
 
 @pytest.mark.parametrize("B", [64, 40, 300])

@@ -32,7 +32,7 @@ def test_cnn_bwd_exact(gpu, B, ipb):
     dpool = torch.randn(B, 9216, generator=g).to(torch.bfloat16)
     s = torch.randint(0, 4, (B, 9216), generator=g)
     pos = torch.rand(B, 9216, generator=g) < 0.7
-    pmask = (s | (pos.long() << 7)).to(torch.uint8)
+    pmask = torch.where(pos, 0x80 | (1 << s), 0).to(torch.uint8)   # cnn_fwd's encoding
     w2 = torch.randn(64, 9, 32, generator=g).to(torch.bfloat16)          # [co][tap][ci]
     w2t = w2.reshape(64, 288).t().contiguous()                             # [tap*32+ci][co]
     nblk = C.cnn_bwd_nblk(B, ipb)
@@ -52,7 +52,7 @@ def test_cnn_bwd_exact(gpu, B, ipb):
     mk = pmask.view(B, 12, 12, 64).long()
     dz2 = torch.zeros(B, 24, 24, 64, dtype=d)
     for sidx in range(4):
-        sel = ((mk & 0x83) == (0x80 | sidx)).to(d)
+        sel = (mk == (0x80 | (1 << sidx))).to(d)
         dz2[:, (sidx >> 1)::2, (sidx & 1)::2, :] = dp * sel
     a1n = a1.to(d).view(B, 26, 26, 32).permute(0, 3, 1, 2)                # NCHW
     dzn = dz2.permute(0, 3, 1, 2)
