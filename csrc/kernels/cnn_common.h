@@ -60,6 +60,19 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group gives the address of row q,
 // columns 4p..4p+3; lane i receives column i of the 4 rows.
+// ReLU / max-pool as single integer VALU ops.  hipcc lowers fmaxf (and x > 0 ? x : 0) on a
+// value it cannot prove canonical -- every MFMA result -- to two v_max_f32 (a NaN-quieting
+// self-max first), and these kernels are VALU-bound where they apply them (64-wide waves
+// take 4 cycles per VALU op on CDNA).  On the bit patterns, a signed integer max against 0
+// IS relu (negative floats are negative integers, -0.0 becomes +0.0), and among positive
+// floats integer order is float order, so the max-pool of relu(x) is relu of the integer
+// max.  (Inline-asm v_max_f32 would do it too, but hipcc inserts no MFMA-result wait states
+// in front of inline asm.)
+__device__ __forceinline__ int fbits(float x) { return __builtin_bit_cast(int, x); }
+__device__ __forceinline__ float relu1(float x) {
+  return __builtin_bit_cast(float, max(fbits(x), 0));
+}
+
 __device__ __forceinline__ s16x4 lds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }

@@ -24,12 +24,13 @@ using namespace cnn;
 
 // ---- cnn_fwd LDS carve (one static array; every offset 16-B aligned) ----
 constexpr int FWD_THREADS = 512;
-constexpr int F_XS = 0;                       // bf16 x [28*28] + zero pad  1600 B
-constexpr int F_A1 = 1600;                    // bf16 a1 image              43264 B
+constexpr int F_X3 = 0;                       // bf16x4 x3[p] = x[p..p+2], 0  6272 B
+constexpr int F_A1 = 6400;                    // bf16 a1 image              43264 B
 constexpr int F_PS = F_A1 + P1 * 64;          // bf16 pooled [144][64]      18432 B
 constexpr int F_MS = F_PS + PP * C2 * 2;      // u8 mask [144][64]          9216 B
 constexpr int F_LUT = F_MS + PP * C2;         // bf16 normalize LUT [256]     512 B
-constexpr int F_TOTAL = F_LUT + 512;          // 73024 B -> 2 workgroups / CU
+constexpr int F_TOTAL = F_LUT + 512;          // 77824 B -> 2 workgroups / CU
+static_assert(2 * F_TOTAL <= 163840 && F_A1 % 128 == 0, "cnn_fwd LDS carve");
 
 template <bool TRAIN>
 __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
     uint8_t* __restrict__ xg, int32_t* __restrict__ ylab) {
   __shared__ __attribute__((aligned(16))) char smem[F_TOTAL];
-  bf16* xs = reinterpret_cast<bf16*>(smem + F_XS);
+  bf16x4* x3 = reinterpret_cast<bf16x4*>(smem + F_X3);
   char* a1s = smem + F_A1;
   bf16* ps = reinterpret_cast<bf16*>(smem + F_PS);
   uint8_t* ms = reinterpret_cast<uint8_t*>(smem + F_MS);
@@ -57,8 +58,12 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   PDM_CHECK(row_u < nrow, "cnn_fwd sample row past the epoch", row_u, nrow);
   const int64_t row = min(row_u, nrow - 1);
   const int64_t src = idx ? (int64_t)idx[row] : row;
-  uint32_t xw = 0;
-  if (tid < 196) xw = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];
+  // pixels 4 tid .. 4 tid + 3, and the next word's first two (the x3 entries need x[p + 2])
+  uint32_t xw = 0, xn = 0;
+  if (tid < 196) {
+    xw = reinterpret_cast<const uint32_t*>(images + src * 784)[tid];
+    xn = reinterpret_cast<const uint32_t*>(images + src * 784)[min(tid + 1, 195)];
+  }
   // the label is a per-lane (vector) load consumed at the very end: a uniform-address
   // scalar load here made wave 0 wait for it (s_waitcnt lgkmcnt(0)) before issuing its
   // weight loads, delaying the first barrier by ~1.7k cycles
@@ -79,32 +84,32 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   __syncthreads();   // normalize LUT ready (the image load keeps flying)
 
   // conv1 as D[co][pixel] = W1[co][tap] . X[tap][pixel] on mfma_f32_16x16x16_bf16:
-  // A = weights (lane row co = i16, k = taps 4g..4g+3, zero past tap 8), B = input
-  // patches (lane col = pixel, k = taps); bias is the initial accumulator.
+  // A = weights (lane row co = i16; k = 4g + j is tap (ky = g, kx = j), zero for g = 3 or
+  // j = 3), B = input patches (lane col = pixel): lane group g reads the x3 entry of pixel
+  // p + 28 g, i.e. the row-ky triple x[p + 28 ky .. + 2] and a zero, in ONE 8-byte read;
+  // bias is the initial accumulator.
   // (the bf16 conversion of the weights happens after the barriers: converting here made
   // every wave wait for its conv1 weight loads before the first barrier)
   float w1v[2][4];
-  int toff[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tap = 4 * g + j;
-    toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;  // -> zero pad entry
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)   // clamped unconditional load (no branch/wait)
-      w1v[mt][j] = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
-  }
+      w1v[mt][j] = w1[(mt * 16 + i16) * 9 + 3 * min(g, 2) + min(j, 2)];
   f32x4 b1v[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
   if (tid < 196) {
-    bf16x4 v = {lut[xw & 0xff], lut[(xw >> 8) & 0xff], lut[(xw >> 16) & 0xff], lut[xw >> 24]};
-    reinterpret_cast<bf16x4*>(xs)[tid] = v;
+    const bf16 v[6] = {lut[xw & 0xff], lut[(xw >> 8) & 0xff], lut[(xw >> 16) & 0xff],
+                       lut[xw >> 24], lut[xn & 0xff], lut[(xn >> 8) & 0xff]};
+    // (entries 782, 783 take two values past the image: finite, and only ever multiplied
+    // into outputs of the virtual columns 26, 27, which are dropped)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x3[4 * tid + i] = bf16x4{v[i], v[i + 1], v[i + 2], bf16{}};
     if (TRAIN) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[tid] = xw;
     if (tid == 0) PDM_STAMP_VAL(9, PDM_CLOCK());   // image landed
-  } else if (tid < 200) {
-    reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};   // zero pad (taps 9..15)
   }
   __syncthreads();
   PDM_STAMP(1);
@@ -125,15 +130,19 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   auto load_wb = [&](int f) {   // fragments 3f .. 3f+2 of the 18 (tap, n-tile) pairs
 #pragma unroll
     for (int e = 3 * f; e < 3 * f + 3; ++e)
+#if defined(PDM_ABL) && PDM_ABL == 4   // timing ablation only: no conv2 weight loads
+      wb[e >> 1][e & 1] = bf16x8{};
+#else
       wb[e >> 1][e & 1] = *reinterpret_cast<const bf16x8*>(
           w2 + ((nh * 32 + (e & 1) * 16 + i16) * 9 + (e >> 1)) * 32 + 8 * g);
+#endif
   };
 
   bf16x4 w1f[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
+    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(g < 3 && j < 3 ? w1v[mt][j] : 0.f);
   // 2. conv1 + bias + ReLU -> LDS a1 image; lane holds 4 consecutive channels of one
   // pixel -> one 8-byte LDS store per 16x16 tile.  Tiles of 16 "virtual pixels" V = 28y + x
   // of the 28-wide x image (x = 26, 27 and y >= 26 computed and dropped): V is the pixel's
@@ -141,9 +150,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   // the a1 store is (V - 2y) * 64 + a per-lane constant.  46 tiles (48 slots) over 8 waves.
   {
     constexpr int TPW = 6;
-    int tb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tb[j] = toff[j] == IMG * IMG ? 0 : toff[j];   // w = 0 there
+    const int rowg = IMG * (g < 3 ? g : 0);   // lane group 3: zero weights, any finite x
     const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);   // mt = 0; mt = 1: ^ 32
     // two rounds of 3 tiles: the 72 conv2 B-fragment registers are live here, and 6 tiles'
     // operands at once would push the kernel past 128 VGPRs (2 workgroups / CU)
@@ -154,9 +161,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #pragma unroll
     for (int k = h; k < h + 3; ++k) {
       vv[k] = (wave + 8 * k) * 16 + i16;
-      const int vc = min(vv[k], IMG * H1 - 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bx[k][j] = xs[vc + tb[j]];
+      bx[k] = x3[min(vv[k], IMG * H1 - 1) + rowg];
     }
 #pragma unroll
     for (int k = h; k < h + 3; ++k) {
@@ -167,9 +172,11 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-        bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
-                    to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
-        if (ok) *reinterpret_cast<bf16x4*>(a1s + (ab ^ (32 * mt))) = o;
+        bf16x4 o = {to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
+                    to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
+        // dropped pixels store into the (not yet used) pooled-output area: no branch
+        const int dst = ok ? F_A1 + (ab ^ (32 * mt)) : F_PS + lane * 8;
+        *reinterpret_cast<bf16x4*>(smem + dst) = o;
       }
     }
     }
@@ -208,15 +215,16 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int co = nh * 32 + j * 16 + i16;
-      float best = fmaxf(acc[j][0], 0.f);
-      int bi = 0;
-#pragma unroll
-      for (int r = 1; r < 4; ++r) {
-        const float v = fmaxf(acc[j][r], 0.f);
-        if (v > best) { best = v; bi = r; }          // first max in (dy, dx) row-major order
-      }
-      ps[pp * C2 + co] = to_bf16(best);
-      ms[pp * C2 + co] = (uint8_t)(best > 0.f ? 0x80 | (1 << bi) : 0);   // one-hot argmax
+      // max-pool of relu = relu of the max, taken on the bit patterns (cnn_common.h relu1);
+      // argmax: first window position (dy, dx row-major) holding it (only used when > 0)
+      const int b0 = fbits(acc[j][0]), b1 = fbits(acc[j][1]), b2 = fbits(acc[j][2]);
+      const int mb = max(max(max(b0, b1), b2), fbits(acc[j][3]));
+      uint32_t oh = b2 == mb ? 4u : 8u;   // selects, last to first (no branches)
+      oh = b1 == mb ? 2u : oh;
+      oh = b0 == mb ? 1u : oh;
+      const bool pos = mb > 0;
+      ps[pp * C2 + co] = to_bf16(__builtin_bit_cast(float, max(mb, 0)));
+      ms[pp * C2 + co] = (uint8_t)(pos ? 0x80u | oh : 0u);   // one-hot argmax
     }
   }
   PDM_STAMP(3);

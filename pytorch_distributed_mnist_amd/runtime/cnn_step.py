@@ -61,7 +61,7 @@ class CnnStep(GpuStepBase):
         self.pmask = torch.empty(cap * 9216, dtype=torch.uint8, device=dev)
         self.xg = torch.empty(B * 784, dtype=torch.uint8, device=dev)
         self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
-        self.splitk_train = choose_splitk(B)
+        self.splitk_train = choose_splitk(B, cap=int(os.environ.get("PDM_SPLITK_CAP", "32")))
         self.splitk_eval = choose_splitk(min(cap, EVAL_CHUNK))
         part_n = max(self.splitk_train * B, self.splitk_eval * EVAL_CHUNK) * 128
         self.part = torch.empty(part_n, dtype=torch.float32, device=dev)
