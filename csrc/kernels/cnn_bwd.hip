@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 }
 
 // ------------------------------------------------------------------ cnn_bwd
-// LDS carve (one static array, 162,688 B -> 1 workgroup / CU):
+// LDS carve (one static array, 163,200 B -> 1 workgroup / CU):
 //   x    bf16 [28*28] + zero pad                                     1600
 //   a1   26x26 px x 32 ch bf16 (a1_off swizzle)                     43264
 //   zero 512 B: target of the dgrad reads whose dz2 row is outside the image
@@ -288,7 +288,8 @@ constexpr int B_Z0 = B_A1 + P1 * 64;            // 44928
 constexpr int B_DZ = B_Z0 + 512;                // 45440 (128-B aligned)
 constexpr int B_W2 = B_DZ + H2 * DS * 128;      // 125312
 constexpr int B_LUT = B_W2 + 9 * C1 * C2 * 2;   // normalize LUT: 256 x bf16    512
-constexpr int B_TOTAL = B_LUT + 512;            // 162688
+constexpr int B_SPARE = B_LUT + 512;           // 512 B target of dropped conv1 stores
+constexpr int B_TOTAL = B_SPARE + 512;          // 163200
 constexpr int B_RED = B_A1;
 constexpr int RED_DB2 = 0;                      // [8 waves][64]
 constexpr int RED_DW1 = RED_DB2 + 8 * C2;       // [4 waves][32 ci][16 taps] (tap 9 = bias)
@@ -309,7 +310,7 @@ static_assert(SL_DB2 == CNN_CONV_SLAB_DB2 && SL_DW1 == CNN_CONV_SLAB_DW1 &&
 // and the scatter's window writes, 1.67-way for the wgrad ds_read_b64_tr_b16 columns
 // (tools/lds_bank_model.py).
 constexpr int W2_CHUNKS = 9 * C1 * C2 * 2 / 16;   // 2304 16-B chunks of W2^T
-constexpr int W2_PER_T = (W2_CHUNKS + BWD_THREADS - 1) / BWD_THREADS;   // 5
+static_assert(W2_CHUNKS % 64 == 0, "W2^T copies in whole 1-KB DMA blocks");
 
 // Stage one image into LDS, ordered so that nothing waits for a load it does not need:
 //   1. issue every global load: x and the conv1 weights first, then (the workgroup's first
@@ -333,7 +334,6 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   const int g = lane >> 4, i16 = lane & 15;
   bf16* xs = reinterpret_cast<bf16*>(smem + B_XS);
   bf16* lut = reinterpret_cast<bf16*>(smem + B_LUT);
-  char* a1s = smem + B_A1;
   // ---- 1. loads
   uint32_t xw = 0;
   if (tid < 196) xw = reinterpret_cast<const uint32_t*>(xg + (int64_t)img * 784)[tid];
@@ -351,12 +351,6 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
-  uint4 wv[W2_PER_T];
-  if (first) {
-#pragma unroll
-    for (int k = 0; k < W2_PER_T; ++k)
-      wv[k] = reinterpret_cast<const uint4*>(w2t)[min(tid + k * BWD_THREADS, W2_CHUNKS - 1)];
-  }
   const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT);
   const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT);
   uint4 d[3];
@@ -366,6 +360,23 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
     const int it = min(tid + k * BWD_THREADS, PP * 8 - 1);   // live W2^T registers to span
     d[k] = dpv[it];
     mk[k] = mkv[it];
+  }
+  // W2^T (first image): straight into its LDS image by LDS-DMA, behind this thread's own
+  // loads; nothing waits for it until the end of the staging, so the normalize barrier and
+  // conv1 no longer wait for 36 KB of weights.  Wave w copies 1-KB blocks w + 8m (8 rows of
+  // 128 B); lane l fills slot l & 7 of row l >> 3 with chunk (l & 7) ^ ((row >> 1) & 7)
+  // (the swizzle goes on the source address: the DMA's LDS side is lane-linear).
+  __builtin_amdgcn_sched_barrier(0);
+  if (first) {
+    const unsigned wbase = lds_addr(smem) + B_W2;
+#pragma unroll
+    for (int m = 0; m < (W2_CHUNKS / 64 + 7) / 8; ++m) {
+      const int blk = wave + 8 * m;
+      if (blk < W2_CHUNKS / 64) {
+        const int row = 8 * blk + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
+        glds16(w2t + row * 64 + ch * 8, wbase + blk * 1024);
+      }
+    }
   }
   // the arithmetic below stays behind the loads (hipcc otherwise hoists it above them and
   // delays the first HBM request)
@@ -381,16 +392,7 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
                                    : B_Z0 + (pix - 2 * H2) * 128;
       *reinterpret_cast<uint4*>(smem + off + (i & 7) * 16) = make_uint4(0, 0, 0, 0);
     }
-    // W2^T image before the barrier: its 20 registers must not live across it (hipcc spills
-    // them there).  Its loads precede dpool / pmask, so this waits for them only.  The
-    // clamped duplicate chunks rewrite the last chunk with the same value.
-#pragma unroll
-    for (int k = 0; k < W2_PER_T; ++k) {
-      const int it = min(tid + k * BWD_THREADS, W2_CHUNKS - 1);
-      const int row = it >> 3, ch = it & 7;
-      *reinterpret_cast<uint4*>(smem + B_W2 + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4)) = wv[k];
-    }
-    __syncthreads();   // LUT + W2^T ready (dpool / pmask keep flying)
+    __syncthreads();   // LUT ready (dpool / pmask / W2^T keep flying)
   }
   // ---- 3. x through the LUT, conv1 recompute
   if (tid < 196) {
@@ -434,9 +436,11 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-      bf16x4 o = {to_bf16(fmaxf(acc[0], 0.f)), to_bf16(fmaxf(acc[1], 0.f)),
-                  to_bf16(fmaxf(acc[2], 0.f)), to_bf16(fmaxf(acc[3], 0.f))};
-      if (ok) *reinterpret_cast<bf16x4*>(a1s + (ab ^ (32 * mt))) = o;
+      bf16x4 o = {to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
+                  to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
+      // dropped pixels store into the spare LDS tail: no branch
+      const int dst = ok ? B_A1 + (ab ^ (32 * mt)) : B_SPARE + lane * 8;
+      *reinterpret_cast<bf16x4*>(smem + dst) = o;
     }
   }
   if (threadIdx.x == 0) PDM_STAMP_VAL(14, PDM_CLOCK());
@@ -490,6 +494,8 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   }
   if (threadIdx.x == 0) PDM_STAMP_VAL(12, PDM_CLOCK());
   if (threadIdx.x == 448) PDM_STAMP_VAL(15, PDM_CLOCK());
+  // the W2^T DMA has landed before the caller's barrier publishes the staging
+  if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // conv2 input gradient for MTP tiles {tile0 + 4k} of 16 virtual pixels V = 28y + x (the

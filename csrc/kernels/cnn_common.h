@@ -73,6 +73,23 @@ __device__ __forceinline__ float relu1(float x) {
   return __builtin_bit_cast(float, max(fbits(x), 0));
 }
 
+// LDS byte address of a __shared__ pointer (the M0 base of an LDS-DMA load)
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// Asynchronous 16-B global -> LDS copy (global_load_lds_dwordx4, no VGPR destination): lane l
+// of the wave writes LDS bytes [lds + 16 l, +16) (wave-uniform lds) from its own gsrc.  Inline
+// asm, so hipcc neither waits for it before every later LDS access (it does for the builtin)
+// nor counts it: the caller waits with s_waitcnt vmcnt(0) before a barrier that publishes
+// the data, and issues it after its own loads (hipcc's counted waits on those then stay
+// correct: they can only over-wait).
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+
 __device__ __forceinline__ s16x4 lds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
