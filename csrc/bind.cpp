@@ -312,6 +312,10 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
   need(b1, at::kFloat, "b1");
   need(b2, at::kFloat, "b2");
   TORCH_CHECK(w1.numel() == 32 * 9 && b1.numel() == 32 && b2.numel() == 64, "conv1/conv2 bias");
+  // staged into LDS as 16-B vectors (cnn_fwd step 0)
+  need_aligned(w1.data_ptr(), 16, "w1");
+  need_aligned(b1.data_ptr(), 16, "b1");
+  need_aligned(b2.data_ptr(), 16, "b2");
   need_min(w2, at::kBFloat16, 64 * 288, "w2");
   need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
   need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");

@@ -29,7 +29,8 @@ constexpr int F_A1 = 6400;                    // bf16 a1 image              4326
 constexpr int F_PS = F_A1 + P1 * 64;          // bf16 pooled [144][64]      18432 B
 constexpr int F_MS = F_PS + PP * C2 * 2;      // u8 mask [144][64]          9216 B
 constexpr int F_LUT = F_MS + PP * C2;         // bf16 normalize LUT [256]     512 B
-constexpr int F_TOTAL = F_LUT + 512;          // 77824 B -> 2 workgroups / CU
+constexpr int F_W = F_LUT + 512;              // fp32 w1 [288] | b1 [32] | b2 [64] 1536 B
+constexpr int F_TOTAL = F_W + 1536;           // 79360 B -> 2 workgroups / CU
 static_assert(2 * F_TOTAL <= 163840 && F_A1 % 128 == 0, "cnn_fwd LDS carve");
 
 template <bool TRAIN>
@@ -50,6 +51,19 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;
   PDM_STAMP(0);
+  // 0. the small conv weights (w1, b1, b2: 384 floats) as 96 16-B loads by waves 4-5, staged
+  // through LDS: per-lane gathers were 18 load instructions in every wave (144 per CU) that
+  // queued in the texture unit in front of the conv1 phase.  Issued first: they do not
+  // depend on the counter, so they land while the image's dependent chain is in flight.
+  float4 wq = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int wt = tid - 256;
+  if (wt >= 0 && wt < 96) {
+    const float4* srcw = wt < 72 ? reinterpret_cast<const float4*>(w1) + wt
+                         : wt < 80 ? reinterpret_cast<const float4*>(b1) + (wt - 72)
+                                   : reinterpret_cast<const float4*>(b2) + (wt - 80);
+    wq = *srcw;
+  }
+  __builtin_amdgcn_sched_barrier(0);
   // 1. gather: the dependent chain (counter -> index -> image row) is issued before
   // anything else so its latency is not queued behind the weight loads.
   // sample row: sampler index (idx), epoch-buffer row (ctr only) or plain row (eval)
@@ -80,8 +94,10 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   // otherwise hold the LUT, and the barrier, back by ~2k cycles)
   bf16* lut = reinterpret_cast<bf16*>(smem + F_LUT);
   if (tid >= 256) lut[tid - 256] = to_bf16(pdm_normalize(tid - 256));
+  float* wl = reinterpret_cast<float*>(smem + F_W);
+  if (wt >= 0 && wt < 96) reinterpret_cast<float4*>(wl)[wt] = wq;
   __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();   // normalize LUT ready (the image load keeps flying)
+  __syncthreads();   // normalize LUT + conv weights ready (the image load keeps flying)
 
   // conv1 as D[co][pixel] = W1[co][tap] . X[tap][pixel] on mfma_f32_16x16x16_bf16:
   // A = weights (lane row co = i16; k = 4g + j is tap (ky = g, kx = j), zero for g = 3 or
@@ -95,12 +111,10 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)   // clamped unconditional load (no branch/wait)
-      w1v[mt][j] = w1[(mt * 16 + i16) * 9 + 3 * min(g, 2) + min(j, 2)];
+      w1v[mt][j] = wl[(mt * 16 + i16) * 9 + 3 * min(g, 2) + min(j, 2)];
   f32x4 b1v[2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  for (int mt = 0; mt < 2; ++mt) b1v[mt] = reinterpret_cast<const f32x4*>(wl + 288)[mt * 4 + g];
   if (tid < 196) {
     const bf16 v[6] = {lut[xw & 0xff], lut[(xw >> 8) & 0xff], lut[(xw >> 16) & 0xff],
                        lut[xw >> 24], lut[xn & 0xff], lut[(xn >> 8) & 0xff]};
@@ -123,7 +137,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   const int nh = wave & 1;
   float b2r[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) b2r[j] = b2[nh * 32 + j * 16 + i16];
+  for (int j = 0; j < 2; ++j) b2r[j] = wl[320 + nh * 32 + j * 16 + i16];
   bf16x8 wb[9][2];
   // issued 3 per conv1 tile below: all 18 at once filled the CU's TA queue (8 waves x 18 KB)
   // and stalled every wave's conv1 issue behind them for ~2.3k cycles
