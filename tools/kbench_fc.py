@@ -24,7 +24,8 @@ torch.cuda.synchronize()
 role = os.environ.get("PDM_FC1BWD_ROLE", "all")
 us = timeit(lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"], st.dpool,
                               st.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
-                              st.metrics.train_view()))
+                              st.metrics.train_view(),
+                              st._fc_update() if st.fuse_fc1 else None))
 print(f"B={B} fc1_bwd role={role}: {us:.2f} us", flush=True)
 if role == "all":
     nb = C.cnn_bwd_nblk(B, choose_ipb(B))
