@@ -632,8 +632,8 @@ __device__ __forceinline__ void dgrad_pass(const char* smem, int tile0, const in
 #endif
 constexpr int DG_MTP = PDM_DG_MTP;       // tiles per dgrad pass on waves 4-7
 constexpr int DG_PFD = PDM_DG_PFD;       // read-ahead distance in (tap, K-half) steps
-static_assert(DG_MTP == 4, "dgrad passes: 3 x 4 tiles per wave (the wgrad waves take pass 2 when "
-              "a workgroup has one image)");
+static_assert(12 % DG_MTP == 0, "dgrad passes: 12 / DG_MTP passes of DG_MTP tiles per wave (the "
+              "wgrad waves take the last pass when a workgroup has one image)");
 static_assert(DG_PFD * (DG_MTP + 2) <= 15, "in-flight LDS reads must fit lgkmcnt");
 
 // ONE: one image per workgroup (B <= CUs).  Its own kernel, so that register allocation of the
@@ -780,11 +780,11 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
         PDM_STAMP(3);
       }
       // one image per workgroup: with its accumulators stored, this wave also takes the
-      // last dgrad pass (tiles 32 + wave + 4k), which balances the two wave groups (the
+      // last dgrad pass (tiles 48 - 4 DG_MTP + wave + 4k), which balances the two wave groups (the
       // wgrad's 360 MFMAs vs the dgrad's 432 + epilogues)
       if constexpr (decltype(one)::value) {
         if (img < B && PDM_ABL != 2)
-          dgrad_pass<DG_MTP, DG_PFD>(smem, 32 + wave, ka1, acc1, t_mf, t_ep);
+          dgrad_pass<DG_MTP, DG_PFD>(smem, 48 - 4 * DG_MTP + wave, ka1, acc1, t_mf, t_ep);
       }
       __syncthreads();
     };
