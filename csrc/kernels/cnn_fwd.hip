@@ -347,15 +347,35 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
   float sx = 0.f;                             // dbfc2 / dbfc1 / loss / correct entry
   double el = 0.0, ec = 0.0;                  // eval metrics (thread 0)
   int en = 0;
+  PDM_STAMP(10);   // head phases in slots 10-15 (cnn_fwd uses 0-9 of the same blocks)
   const float2 bias = reinterpret_cast<const float2*>(bf1)[j];
+  // fc2 weights of this lane's two hidden units, loaded once up front and used by both the
+  // logits and dh (reloading them for dh was another memory round trip in the chain)
+  float2 w2v[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) w2v[c] = reinterpret_cast<const float2*>(wf2 + c * HID)[j];
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int row = grp * HEAD_ROWS + r;
     const bool valid = row < B;
+    const int y = valid ? ylab[row] : 0;
     float2 h = bias;
-    {
+    const int rc = min(row, B - 1);
+    if (S == 32) {
+      // the training split count at B <= 256: every partial load in flight at once (one
+      // memory round trip -- the partials come from other XCDs' writes, ~1.4 us away)
+      float2 u[32];
+#pragma unroll
+      for (int q = 0; q < 32; ++q)
+        u[q] = reinterpret_cast<const float2*>(part + ((int64_t)q * B + rc) * HID)[j];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        h.x += u[q].x;
+        h.y += u[q].y;
+      }
+    } else {
       // split-K partials in batches of 16 loads in flight (clamped addresses + selects),
       // summed in split order
-      const int rc = min(row, B - 1);
       for (int s0 = 0; s0 < S; s0 += 16) {
         float2 u[16];
 #pragma unroll
@@ -371,19 +391,17 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
         }
       }
     }
+    PDM_STAMP(11);
     h.x = valid ? fmaxf(h.x, 0.f) : 0.f;
     h.y = valid ? fmaxf(h.y, 0.f) : 0.f;
 
     float lg[NCLS];
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) {
-      const float2 w = reinterpret_cast<const float2*>(wf2 + c * HID)[j];
-      lg[c] = wave_sum(fmaf(h.y, w.y, h.x * w.x)) + bf2[c];
-    }
-    const int y = valid ? ylab[row] : 0;
+    for (int c = 0; c < NCLS; ++c) lg[c] = wave_sum(fmaf(h.y, w2v[c].y, h.x * w2v[c].x)) + bf2[c];
     float prob[NCLS];
     int correct;
     const float loss = row_xent<NCLS>(lg, y, prob, correct);
+    PDM_STAMP(12);
     if (j == 0) {
       red[r][0] = valid ? loss : 0.f;
       red[r][1] = valid ? (float)correct : 0.f;
@@ -397,9 +415,8 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
       float2 dhv = make_float2(0.f, 0.f);
 #pragma unroll
       for (int c = 0; c < NCLS; ++c) {
-        const float2 w = reinterpret_cast<const float2*>(wf2 + c * HID)[j];
-        dhv.x = fmaf(dl[c], w.x, dhv.x);
-        dhv.y = fmaf(dl[c], w.y, dhv.y);
+        dhv.x = fmaf(dl[c], w2v[c].x, dhv.x);
+        dhv.y = fmaf(dl[c], w2v[c].y, dhv.y);
       }
       dhv.x = h.x > 0.f ? dhv.x : 0.f;
       dhv.y = h.y > 0.f ? dhv.y : 0.f;
@@ -415,6 +432,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
         for (int c = 0; c < NCLS; ++c) dls[r][c] = dl[c];
       }
     }
+    PDM_STAMP(13);
     __syncthreads();
     if (TRAIN) {
 #pragma unroll
@@ -440,6 +458,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
         en += (grp * HEAD_ROWS + i < B);
       }
     }
+    PDM_STAMP(14);
     __syncthreads();   // LDS is rewritten by the next row group
   }
   if (!TRAIN) {
@@ -457,6 +476,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
   else if (tid >= 16 && tid < 16 + HID) out[NCLS * HID + NCLS + tid - 16] = sx;
   else if (tid == 254 || tid == 255) out[HEAD_SLAB - 2 + (tid - 254)] = sx;
   pdm_bump_counters(c0, c1, c2);
+  PDM_STAMP(15);
 }
 
 }  // namespace

@@ -32,6 +32,12 @@ for which, names in (("fwd", ["start", "gathered(barrier)", "conv1(barrier)", "c
         print(f"   {nm:22s} {med[i]:9.0f} {mx[i]:9.0f}")
     print("   block start skew (cycles):", (st[:, 0] - t0).max().item(),
           " last end:", (st[:, n - 1] - t0).max().item())
+    if which == "fwd" and B <= 256:
+        hs = st[:B // 4, 10:16]            # cnn_head, blocks 0 .. B/4 - 1 (one row group each)
+        hb = hs[:, 0:1]
+        hm = (hs - hb).median(dim=0).values
+        print("   head: partials summed / xent / dh stored / slab acc / end (rel, median):",
+              " ".join(f"{v:.0f}" for v in hm[1:].tolist()))
     if which == "fwd":
         print("   image load issued (rel)", (st[:, 8] - st[:, 0]).median().item(),
               " image landed (rel)", (st[:, 9] - st[:, 0]).median().item())
