@@ -42,6 +42,17 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ------------------------------------------------------------------ fc1_bwd
+// diagnostic stamps (PDM_STAMPS builds; tools/stamps_fc.py): dX tile t -> row t, slots 0-3;
+// dW tile b -> row b, slots 8-13 (cnn_bwd overwrites them, so fc1_bwd is stamped alone)
+#ifdef PDM_STAMPS
+#define FC_STAMP(row, slot)                                                         \
+  do {                                                                              \
+    if (threadIdx.x == 0 && (row) < 256)                                            \
+      pdm_stamps[(row) * 16 + (slot)] = __builtin_amdgcn_s_memtime();              \
+  } while (0)
+#else
+#define FC_STAMP(row, slot) do { } while (0)
+#endif
 constexpr int DW_TILES = FEAT / 64;  // 144
 constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
 constexpr int DX_COLS = 384;         // dX tile: 32 batch rows x 384 features per workgroup
@@ -73,6 +84,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     // dh^T A fragments) is loaded with every load in flight at once, and the next chunk's
     // loads are issued before the current chunk's MFMAs.
     const int k0 = bid * 64;
+    FC_STAMP(bid, 8);
     f32x4 acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -125,6 +137,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
         for (int kk = 0; kk < DWC / 32; ++kk) ac[mt][kk] = a[mt][kk];
       __syncthreads();
+      FC_STAMP(bid, c0 == 0 ? 9 : 10);   // chunk landed in LDS
       if (c0 + DWC < ldt) load_chunk(c0 + DWC);
       __builtin_amdgcn_sched_barrier(0);   // next chunk's loads stay ahead of this chunk's MFMAs
       const int nk = min(DWC / 32, (ldt - c0) / 32);
@@ -143,6 +156,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         }
       }
     }
+    FC_STAMP(bid, 11);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -172,6 +186,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
             fcu.shadow[q] = to_bf16(p);
           }
     }
+    FC_STAMP(bid, 13);
     return;
   }
 
@@ -186,6 +201,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     // 8), and every XCD owns 1/8 of the feature range, so each XCD's L2 holds only its 1/8
     // of W1^T.
     const int t = bid - DW_TILES;
+    FC_STAMP(t, 0);
     constexpr int TPX = DX_TILES / NXCD;                 // feature tiles per XCD
     const int xcd = t % NXCD, loc = t / NXCD;
     const int b0 = (loc / TPX) * 32;
@@ -205,6 +221,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     // keep every load above this point: the scheduler would otherwise interleave them
     // with the MFMAs behind per-load waits
     __builtin_amdgcn_sched_barrier(0);
+    FC_STAMP(t, 1);
     f32x4 acc[DX_FT][2];
 #pragma unroll
     for (int ft = 0; ft < DX_FT; ++ft)
@@ -217,6 +234,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
         for (int bt = 0; bt < 2; ++bt)
           acc[ft][bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ft][ks], hb[bt][ks], acc[ft][bt], 0, 0, 0);
+    FC_STAMP(t, 2);
 #pragma unroll
     for (int bt = 0; bt < 2; ++bt) {
       const int row = b0 + bt * 16 + i16;
@@ -229,6 +247,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         }
       }
     }
+    FC_STAMP(t, 3);
     return;
   }
 
