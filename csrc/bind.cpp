@@ -241,6 +241,10 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
       s.shadow_t = ptr<__bf16>(sh);
     }
     s.tonly = (t.size() > 6 && !t[6].is_none() && t[6].cast<bool>()) ? 1 : 0;
+    s.tfrag = (t.size() > 7 && !t[7].is_none() && t[7].cast<bool>()) ? 1 : 0;
+    if (s.tfrag)
+      TORCH_CHECK(s.shadow_t != nullptr && s.rows % 32 == 0 && s.cols % 16 == 0,
+                  "a fragment-major shadow_t needs rows % 32 == 0 and cols % 16 == 0");
     if (s.tonly) {
       TORCH_CHECK(s.shadow != nullptr && s.shadow_t != nullptr && s.slab == nullptr,
                   "a transpose-only segment needs shadow and shadow_t and no slab");

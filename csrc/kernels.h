@@ -46,7 +46,19 @@ struct OptSeg {
   // transpose-only segment: no update; shadow_t is re-derived from shadow (the update ran
   // elsewhere, e.g. fused into cnn_bwd at world size 1)
   int32_t tonly;
+  // shadow_t layout: 0 = row-major [cols][rows]; 1 = MFMA-fragment-major (rows % 32 == 0,
+  // cols % 16 == 0): the 16 x 32 A fragment (cols 16 fb .., rows 32 ks ..) is one 1-KB block,
+  // lane (g, i) holding rows 32 ks + 8 g .. + 7 of col 16 fb + i -- a wave's fragment load
+  // is then 8 whole cache lines instead of 16 half lines (fc1_bwd's dX tiles)
+  int32_t tfrag;
 };
+
+// offset of element (row, col) of a [rows][cols] matrix in its transposed bf16 copy
+__host__ __device__ inline int64_t shadow_t_pos(int32_t tfrag, int32_t rows, int64_t row, int64_t col) {
+  if (!tfrag) return col * rows + row;
+  return (((col >> 4) * (rows >> 5) + (row >> 5)) * 64 + ((row >> 3) & 3) * 16 + (col & 15)) * 8 +
+         (row & 7);
+}
 
 struct OptArgs {
   float* p;

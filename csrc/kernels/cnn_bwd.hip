@@ -215,8 +215,8 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
             dh + (int64_t)(b0 + bt * 16 + i16) * HID + 32 * ks + 8 * g);
 #pragma unroll
       for (int ft = 0; ft < DX_FT; ++ft)
-        wa[ft][ks] = *reinterpret_cast<const bf16x8*>(
-            wf1t + (int64_t)(f0 + ft * 16 + i16) * HID + 32 * ks + 8 * g);
+        wa[ft][ks] = *reinterpret_cast<const bf16x8*>(     // fragment-major W1^T (kernels.h)
+            wf1t + ((int64_t)(((f0 >> 4) + ft) * (HID / 32) + ks) * 64 + lane) * 8);
     }
     // keep every load above this point: the scheduler would otherwise interleave them
     // with the MFMAs behind per-load waits

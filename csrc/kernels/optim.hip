@@ -66,11 +66,12 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 8;
     const int col = tc0 + c;
     if (col < s.cols) {
-      const int64_t base = (int64_t)col * s.rows + tr0 + rr;
+      const int64_t base = shadow_t_pos(s.tfrag, s.rows, tr0 + rr, col);
       if (tr0 + rr + 8 <= s.rows && (base & 7) == 0) {
         *reinterpret_cast<bf16x8*>(s.shadow_t + base) = *reinterpret_cast<const bf16x8*>(&tt[c][rr]);
       } else {
-        for (int j = 0; j < 8 && tr0 + rr + j < s.rows; ++j) s.shadow_t[base + j] = tt[c][rr + j];
+        for (int j = 0; j < 8 && tr0 + rr + j < s.rows; ++j)
+          s.shadow_t[shadow_t_pos(s.tfrag, s.rows, tr0 + rr + j, col)] = tt[c][rr + j];
       }
     }
     return;
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       if (KIND == OPT_ADAM) V[e] = v;
       const bf16 hb = to_bf16(p);
       if (s.shadow) s.shadow[e] = hb;
-      if (s.shadow_t) s.shadow_t[(int64_t)(e % s.cols) * s.rows + e / s.cols] = hb;
+      if (s.shadow_t) s.shadow_t[shadow_t_pos(s.tfrag, s.rows, e / s.cols, e % s.cols)] = hb;
     }
     return;
   }
@@ -230,11 +231,12 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 8;
   const int col = tc0 + c;
   if (col < s.cols) {
-    const int64_t base = (int64_t)col * s.rows + tr0 + rr;
+    const int64_t base = shadow_t_pos(s.tfrag, s.rows, tr0 + rr, col);
     if (tr0 + rr + 8 <= s.rows && (base & 7) == 0) {
       *reinterpret_cast<bf16x8*>(s.shadow_t + base) = *reinterpret_cast<const bf16x8*>(&tile[c][rr]);
     } else {
-      for (int j = 0; j < 8 && tr0 + rr + j < s.rows; ++j) s.shadow_t[base + j] = tile[c][rr + j];
+      for (int j = 0; j < 8 && tr0 + rr + j < s.rows; ++j)
+        s.shadow_t[shadow_t_pos(s.tfrag, s.rows, tr0 + rr + j, col)] = tile[c][rr + j];
     }
   }
 }
