@@ -51,13 +51,23 @@ struct OptSeg {
   // lane (g, i) holding rows 32 ks + 8 g .. + 7 of col 16 fb + i -- a wave's fragment load
   // is then 8 whole cache lines instead of 16 half lines (fc1_bwd's dX tiles)
   int32_t tfrag;
+  int32_t sfrag;       // shadow layout: 0 = row-major, 1 = fragment-major (frag_pos, m = row)
 };
 
-// offset of element (row, col) of a [rows][cols] matrix in its transposed bf16 copy
+// MFMA-fragment-major offset of element (m, k) of an [M][K] bf16 operand (K % 32 == 0,
+// M % 16 == 0): the 16 x 32 fragment (m >> 4, k >> 5) is one 512-element block and lane
+// ((k >> 3) & 3) * 16 + (m & 15) of a 16x16x32 MFMA operand load holds its 8 k-values --
+// a wave's fragment load reads 1 KB contiguous (8 whole cache lines)
+__host__ __device__ inline int64_t frag_pos(int64_t m, int64_t k, int32_t K) {
+  return (((m >> 4) * (K >> 5) + (k >> 5)) * 64 + ((k >> 3) & 3) * 16 + (m & 15)) * 8 + (k & 7);
+}
+// offset of element (row, col) of a [rows][cols] matrix in its bf16 copy (sfrag: fragment-
+// major with m = row) and in its transposed copy (tfrag: fragment-major with m = col)
+__host__ __device__ inline int64_t shadow_pos(int32_t sfrag, int32_t cols, int64_t row, int64_t col) {
+  return sfrag ? frag_pos(row, col, cols) : row * cols + col;
+}
 __host__ __device__ inline int64_t shadow_t_pos(int32_t tfrag, int32_t rows, int64_t row, int64_t col) {
-  if (!tfrag) return col * rows + row;
-  return (((col >> 4) * (rows >> 5) + (row >> 5)) * 64 + ((row >> 3) & 3) * 16 + (col & 15)) * 8 +
-         (row & 7);
+  return tfrag ? frag_pos(col, row, rows) : col * rows + row;
 }
 
 struct OptArgs {

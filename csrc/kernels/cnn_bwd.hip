@@ -172,19 +172,33 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       // by the optimizer launch).  Same op order as the optimizer kernel: same bits.
       using namespace optim_detail;
       const Hyper h = make_hyper<OPT_SGD>(fcu);
+      // the bf16 copy is fragment-major (fc1_fwd's B operand, kernels.h frag_pos): this tile
+      // is 8 n-tiles x 2 k-steps of 1-KB blocks, assembled in LDS and stored as 16-B chunks
+      __syncthreads();   // every wave's last reads of the pool tile are done
+      bf16* fr = reinterpret_cast<bf16*>(tile);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
-            const int64_t q = (int64_t)(wave * 32 + mt * 16 + 4 * g + r) * FEAT + k0 + 16 * nt + i16;
+            const int n = wave * 32 + mt * 16 + 4 * g + r, kl = 16 * nt + i16;
+            const int64_t q = (int64_t)n * FEAT + k0 + kl;
             float m = fmv[mt][r][nt], v = 0.f;
             const float p = update<OPT_SGD>(fpv[mt][r][nt], acc[mt][nt][r], m, v, h, fcu.grad_scale);
             fcu.p[q] = p;
             fcu.m[q] = m;
-            fcu.shadow[q] = to_bf16(p);
+            fr[(((n >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (n & 15)) * 8 + (kl & 7)] =
+                to_bf16(p);
           }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = tid + 256 * u, blk = c >> 6;   // blk = n-tile * 2 + k-step
+        *reinterpret_cast<uint4*>(fcu.shadow + ((int64_t)((blk >> 1) * (FEAT / 32) + (k0 >> 5) +
+                                                          (blk & 1)) * 64 + (c & 63)) * 8) =
+            reinterpret_cast<const uint4*>(fr)[c];
+      }
     }
     FC_STAMP(bid, 13);
     return;

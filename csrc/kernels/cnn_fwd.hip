@@ -285,8 +285,10 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
   const int r0 = min(b0 + rl, B - 1), r1 = min(b0 + 16 + rl, B - 1);
   const bf16* pa0 = pool + (int64_t)r0 * FEAT + kbeg + kg;
   const bf16* pa1 = pool + (int64_t)r1 * FEAT + kbeg + kg;
-  const bf16* pb0 = wf1 + (int64_t)(n0 + rl) * FEAT + kbeg + kg;
-  const bf16* pb1 = wf1 + (int64_t)(n0 + 16 + rl) * FEAT + kbeg + kg;
+  // W1 is fragment-major (kernels.h frag_pos): the 16 x 32 fragment (n-tile, k-step) is
+  // one 1-KB block and this lane's 16 B sit at lane * 8 in it
+  const bf16* pb0 = wf1 + ((int64_t)((n0 >> 4) * (FEAT / 32) + (kbeg >> 5)) * 64 + lane) * 8;
+  const bf16* pb1 = pb0 + (int64_t)(FEAT / 32) * 512;
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -300,8 +302,8 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
     for (int i = 0; i < FC1_KB; ++i) {
       a0[i] = *reinterpret_cast<const bf16x8*>(pa0 + kb + 32 * i);
       a1[i] = *reinterpret_cast<const bf16x8*>(pa1 + kb + 32 * i);
-      w0[i] = *reinterpret_cast<const bf16x8*>(pb0 + kb + 32 * i);
-      w1[i] = *reinterpret_cast<const bf16x8*>(pb1 + kb + 32 * i);
+      w0[i] = *reinterpret_cast<const bf16x8*>(pb0 + (kb / 32 + i) * 512);
+      w1[i] = *reinterpret_cast<const bf16x8*>(pb1 + (kb / 32 + i) * 512);
     }
     __builtin_amdgcn_sched_barrier(0);   // all loads of the batch before its MFMAs
 #pragma unroll

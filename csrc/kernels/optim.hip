@@ -53,13 +53,14 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const int r = threadIdx.x >> 3, c8 = (threadIdx.x & 7) * 8;
     const int row = tr0 + r, col0 = tc0 + c8;
     if (row < s.rows && col0 < s.cols) {
-      const int64_t e = (int64_t)row * s.cols + col0;
+      const int64_t e = shadow_pos(s.sfrag, s.cols, row, col0);
       if (col0 + 8 <= s.cols && (e & 7) == 0) {
         const bf16x8 hb = *reinterpret_cast<const bf16x8*>(s.shadow + e);
 #pragma unroll
         for (int j = 0; j < 8; ++j) tt[c8 + j][r] = hb[j];
       } else {
-        for (int j = 0; j < 8 && col0 + j < s.cols; ++j) tt[c8 + j][r] = s.shadow[e + j];
+        for (int j = 0; j < 8 && col0 + j < s.cols; ++j)
+          tt[c8 + j][r] = s.shadow[shadow_pos(s.sfrag, s.cols, row, col0 + j)];
       }
     }
     __syncthreads();
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       M[e] = m;
       if (KIND == OPT_ADAM) V[e] = v;
       const bf16 hb = to_bf16(p);
-      if (s.shadow) s.shadow[e] = hb;
+      if (s.shadow) s.shadow[shadow_pos(s.sfrag, s.cols, e / s.cols, e % s.cols)] = hb;
       if (s.shadow_t) s.shadow_t[shadow_t_pos(s.tfrag, s.rows, e / s.cols, e % s.cols)] = hb;
     }
     return;
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
           *reinterpret_cast<float4*>(V + e + 4 * q) =
               make_float4(vv[4 * q], vv[4 * q + 1], vv[4 * q + 2], vv[4 * q + 3]);
       }
-      if (s.shadow) *reinterpret_cast<bf16x8*>(s.shadow + e) = hb;
+      if (s.shadow) *reinterpret_cast<bf16x8*>(s.shadow + shadow_pos(s.sfrag, s.cols, row, col0)) = hb;
     } else {
       for (int j = 0; j < 8 && col0 + j < s.cols; ++j) {
         const int64_t ej = e + j;
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
         M[ej] = m;
         if (KIND == OPT_ADAM) V[ej] = v;
         const bf16 hb = to_bf16(p);
-        if (s.shadow) s.shadow[ej] = hb;
+        if (s.shadow) s.shadow[shadow_pos(s.sfrag, s.cols, row, col0 + j)] = hb;
         tile[c8 + j][r] = hb;
       }
     }

@@ -32,13 +32,18 @@ from .gpu_step import GpuStepBase
 EVAL_CHUNK = 2048
 
 
+def frag_major(w: torch.Tensor) -> torch.Tensor:
+    """[M][K] -> the MFMA-fragment-major layout (csrc/kernels.h frag_pos): the 16 x 32
+    fragment (m // 16, k // 32) is one 512-element block in which lane
+    ((k // 8) % 4) * 16 + m % 16 holds its 8 consecutive k.  Flat 1-D result."""
+    m, k = w.shape
+    t = w.reshape(m // 16, 16, k // 32, 4, 8)                  # [mb][i][kb][g][j]
+    return t.permute(0, 2, 3, 1, 4).contiguous().reshape(-1)   # [mb][kb][g][i][j]
+
+
 def frag_major_t(w: torch.Tensor) -> torch.Tensor:
-    """[rows][cols] -> its transpose in the MFMA-fragment-major layout (csrc/kernels.h
-    shadow_t_pos, tfrag = 1): block (col // 16, row // 32) of 512 elements, lane
-    ((row // 8) % 4) * 16 + col % 16 holding rows 8 consecutive rows.  Flat 1-D result."""
-    rows, cols = w.shape
-    t = w.t().reshape(cols // 16, 16, rows // 32, 4, 8)        # [fb][i][ks][g][j]
-    return t.permute(0, 2, 3, 1, 4).contiguous().reshape(-1)   # [fb][ks][g][i][j]
+    """The transpose of [rows][cols] in the fragment-major layout (kernels.h shadow_t_pos)."""
+    return frag_major(w.t())
 
 
 def choose_splitk(B: int, cap: int = 32, target_blocks: int = 256) -> int:
@@ -124,7 +129,7 @@ class CnnStep(GpuStepBase):
     def refresh_shadows(self) -> None:
         """Re-derive the bf16 weight copies from the fp32 master weights."""
         w1 = self.arena.param("fc1.weight").reshape(128, 9216)
-        self.wf1.copy_(w1.reshape(-1).to(torch.bfloat16))
+        self.wf1.copy_(frag_major(w1.to(torch.bfloat16)))
         self.wf1t.copy_(frag_major_t(w1.to(torch.bfloat16)))
         w2 = self.arena.param("conv2.weight").reshape(64, 288)
         self.w2.copy_(w2.reshape(-1).to(torch.bfloat16))
@@ -136,8 +141,9 @@ class CnnStep(GpuStepBase):
         for p in spec.params:
             off = spec.offset(p.name)
             if p.name == "fc1.weight":
-                # W1^T in the MFMA-fragment-major layout fc1_bwd's dX tiles read (kernels.h)
-                segs.append((off, 128, 9216, self.wf1, self.wf1t, None, False, True))
+                # W1 and W1^T in the MFMA-fragment-major layout fc1_fwd / fc1_bwd's dX tiles
+                # read (kernels.h frag_pos)
+                segs.append((off, 128, 9216, self.wf1, self.wf1t, None, False, True, True))
             elif p.name == "conv2.weight":
                 segs.append((off, 64, 288, self.w2, self.w2t))
             else:
@@ -176,7 +182,7 @@ class CnnStep(GpuStepBase):
                 name = by_off.get(sg[0])
                 if name is None and self.fuse_fc1 and sg[0] == fc1_off:
                     # updated by fc1_bwd: only W1^T = transpose(W1) is left to write
-                    plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True, True))
+                    plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True, True, True))
                 elif name is None:
                     plain.append(sg)
                 else:

@@ -22,8 +22,11 @@ def _pair(arch, kind, gpu):
     return arenas, opts
 
 
+@pytest.mark.parametrize("frag", [False, True])
 @pytest.mark.parametrize("kind", ["adam", "sgd"])
-def test_optim_kernel_matches_cpu(gpu, kind):
+def test_optim_kernel_matches_cpu(gpu, kind, frag):
+    """frag: fc1.weight's bf16 copies in the MFMA-fragment-major layouts the CNN step uses
+    (kernels.h frag_pos), else row-major."""
     from pytorch_distributed_mnist_amd.ops import _ext
     C = _ext.require()
     (ac, ag), (oc, og) = _pair("cnn", kind, gpu)
@@ -35,7 +38,7 @@ def test_optim_kernel_matches_cpu(gpu, kind):
     sht_fc1 = torch.empty(9216 * 128, dtype=torch.bfloat16, device=gpu)
     sh_c2 = torch.empty(64 * 288, dtype=torch.bfloat16, device=gpu)
     sht_c2 = torch.empty(288 * 64, dtype=torch.bfloat16, device=gpu)
-    segs = [(0, 1, off_fc1, None, None), (off_fc1, 128, 9216, sh_fc1, sht_fc1),
+    segs = [(0, 1, off_fc1, None, None), (off_fc1, 128, 9216, sh_fc1, sht_fc1, None, False, frag, frag),
             (off_fc1 + 128 * 9216, 1, off_c2 - off_fc1 - 128 * 9216, None, None),
             (off_c2, 64, 288, sh_c2, sht_c2),
             (off_c2 + 64 * 288, 1, n - off_c2 - 64 * 288, None, None)]
@@ -58,7 +61,13 @@ def test_optim_kernel_matches_cpu(gpu, kind):
     torch.cuda.synchronize()
     assert torch.allclose(ag.params.cpu(), ac.params, atol=1e-6, rtol=1e-5)
     w = ag.params[off_fc1:off_fc1 + 128 * 9216]
-    assert torch.equal(sh_fc1, w.to(torch.bfloat16))
-    assert torch.equal(sht_fc1.view(9216, 128), w.view(128, 9216).t().to(torch.bfloat16))
+    if frag:
+        from pytorch_distributed_mnist_amd.runtime.cnn_step import frag_major, frag_major_t
+        wb = w.view(128, 9216).to(torch.bfloat16)
+        assert torch.equal(sh_fc1, frag_major(wb))
+        assert torch.equal(sht_fc1, frag_major_t(wb))
+    else:
+        assert torch.equal(sh_fc1, w.to(torch.bfloat16))
+        assert torch.equal(sht_fc1.view(9216, 128), w.view(128, 9216).t().to(torch.bfloat16))
     w2 = ag.params[off_c2:off_c2 + 64 * 288]
     assert torch.equal(sht_c2.view(288, 64), w2.view(64, 288).t().to(torch.bfloat16))
