@@ -107,8 +107,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int kk = 0; kk < DWC / 32; ++kk)
-          a[mt][kk] = *reinterpret_cast<const bf16x8*>(
-              dht + (int64_t)(wave * 32 + mt * 16 + i16) * ldt + min(c0 + 32 * kk, ldt - 32) + 8 * g);
+          a[mt][kk] = *reinterpret_cast<const bf16x8*>(   // fragment-major dh^T (frag_pos)
+              dht + ((int64_t)((wave * 2 + mt) * (ldt / 32) + (min(c0 + 32 * kk, ldt - 32) >> 5)) * 64 +
+                     lane) * 8);
     };
     load_chunk(0);
     // fused update (fcu.kind >= 0): this tile's fp32 weights and momentum, issued behind the
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
       for (int bt = 0; bt < 2; ++bt)
         hb[bt][ks] = *reinterpret_cast<const bf16x8*>(
-            dh + (int64_t)(b0 + bt * 16 + i16) * HID + 32 * ks + 8 * g);
+            dh + ((int64_t)(((b0 >> 4) + bt) * (HID / 32) + ks) * 64 + lane) * 8);   // frag_pos
 #pragma unroll
       for (int ft = 0; ft < DX_FT; ++ft)
         wa[ft][ks] = *reinterpret_cast<const bf16x8*>(     // fragment-major W1^T (kernels.h)

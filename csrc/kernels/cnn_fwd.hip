@@ -424,9 +424,11 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
       dhv.y = h.y > 0.f ? dhv.y : 0.f;
       // row < ldt always: rows >= B write zeros (GEMM padding)
       const bf16x2 o = {to_bf16(dhv.x), to_bf16(dhv.y)};
-      dht[(int64_t)(2 * j) * ldt + row] = o[0];
-      dht[(int64_t)(2 * j + 1) * ldt + row] = o[1];
-      *reinterpret_cast<bf16x2*>(dh + (int64_t)row * HID + 2 * j) = o;
+      // both copies fragment-major (kernels.h frag_pos), the layouts fc1_bwd's dW (dh^T: m =
+      // hidden unit, k = batch row) and dX (dh: m = batch row, k = hidden unit) tiles load
+      dht[frag_pos(2 * j, row, ldt)] = o[0];
+      dht[frag_pos(2 * j + 1, row, ldt)] = o[1];
+      *reinterpret_cast<bf16x2*>(dh + frag_pos(row, 2 * j, HID)) = o;
       reinterpret_cast<float2*>(hs[r])[j] = h;
       reinterpret_cast<float2*>(dhs[r])[j] = dhv;
       if (j == 0) {

@@ -5,7 +5,7 @@ fed to the reference exactly, so only fp32-vs-fp64 summation order differs."""
 import pytest
 import torch
 
-from pytorch_distributed_mnist_amd.runtime.cnn_step import frag_major_t
+from pytorch_distributed_mnist_amd.runtime.cnn_step import frag_major, frag_major_t
 
 pytestmark = pytest.mark.gpu
 
@@ -96,8 +96,9 @@ def test_fc1_bwd_exact(gpu, B):
     gbf2 = torch.zeros(10, device=gpu)
     gbf1 = torch.zeros(128, device=gpu)
     metrics = torch.zeros(3, dtype=torch.float64, device=gpu)
-    # W1^T in the MFMA-fragment-major layout the dX tiles read (kernels.h shadow_t_pos)
-    C.fc1_bwd(dh.to(gpu), dht.to(gpu), ldt, pool.to(gpu), frag_major_t(w1).to(gpu), B, gwf1,
+    # dh, dh^T and W1^T in the MFMA-fragment-major layouts (kernels.h frag_pos) the kernel reads
+    C.fc1_bwd(frag_major(dh).to(gpu), frag_major(dht).to(gpu), ldt, pool.to(gpu),
+              frag_major_t(w1).to(gpu), B, gwf1,
               dpool, head_slab.to(gpu), gwf2, gbf2, gbf1, metrics)
     torch.cuda.synchronize()
     d = torch.float64
