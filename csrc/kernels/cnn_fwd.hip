@@ -147,8 +147,8 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #if defined(PDM_ABL) && PDM_ABL == 4   // timing ablation only: no conv2 weight loads
       wb[e >> 1][e & 1] = bf16x8{};
 #else
-      wb[e >> 1][e & 1] = *reinterpret_cast<const bf16x8*>(
-          w2 + ((nh * 32 + (e & 1) * 16 + i16) * 9 + (e >> 1)) * 32 + 8 * g);
+      wb[e >> 1][e & 1] = *reinterpret_cast<const bf16x8*>(   // fragment-major W2 (frag_pos)
+          w2 + ((int64_t)((nh * 2 + (e & 1)) * 9 + (e >> 1)) * 64 + lane) * 8);
 #endif
   };
 

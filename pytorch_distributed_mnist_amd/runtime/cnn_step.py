@@ -132,7 +132,7 @@ class CnnStep(GpuStepBase):
         self.wf1.copy_(frag_major(w1.to(torch.bfloat16)))
         self.wf1t.copy_(frag_major_t(w1.to(torch.bfloat16)))
         w2 = self.arena.param("conv2.weight").reshape(64, 288)
-        self.w2.copy_(w2.reshape(-1).to(torch.bfloat16))
+        self.w2.copy_(frag_major(w2.to(torch.bfloat16)))
         self.w2t.copy_(w2.t().contiguous().reshape(-1).to(torch.bfloat16))
 
     def optimizer_segments(self):
@@ -145,7 +145,9 @@ class CnnStep(GpuStepBase):
                 # read (kernels.h frag_pos)
                 segs.append((off, 128, 9216, self.wf1, self.wf1t, None, False, True, True))
             elif p.name == "conv2.weight":
-                segs.append((off, 64, 288, self.w2, self.w2t))
+                # W2 fragment-major (cnn_fwd's conv2 B operand), W2^T row-major (cnn_bwd's
+                # LDS image)
+                segs.append((off, 64, 288, self.w2, self.w2t, None, False, False, True))
             else:
                 segs.append((off, 1, p.numel, None, None))
         return segs
@@ -186,8 +188,9 @@ class CnnStep(GpuStepBase):
                 elif name is None:
                     plain.append(sg)
                 else:
-                    slab_segs.append(tuple(sg) +
-                                     ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),))
+                    sg = tuple(sg) + (None,) * (9 - len(sg))
+                    slab_segs.append(sg[:5] + ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),) +
+                                     sg[6:])
             # slab segments first: their workgroups (a 256-deep reduction each) are
             # dispatched before the streaming fc updates instead of forming the tail
             segs = slab_segs + plain
