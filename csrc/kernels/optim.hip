@@ -50,7 +50,12 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     __shared__ __attribute__((aligned(16))) bf16 tt[TC][TR + 8];
     const int tiles_c = (s.cols + TC - 1) / TC;
     const int tr0 = (lb / tiles_c) * TR, tc0 = (lb % tiles_c) * TC;
-    const int r = threadIdx.x >> 3, c8 = (threadIdx.x & 7) * 8;
+    // thread -> (row, 8 consecutive cols).  A fragment-major shadow holds this 32 x 64 tile
+    // as two runs of 2 KB (n-tile, two k-steps): thread t reads the t-th 16-B chunk of them
+    // (its (row, cols) follow from frag_pos), so the wave's loads stay whole-line.
+    const int t = threadIdx.x;
+    const int r = s.sfrag ? 16 * (t >> 7) + (t & 15) : t >> 3;
+    const int c8 = s.sfrag ? 32 * ((t >> 6) & 1) + 8 * ((t >> 4) & 3) : (t & 7) * 8;
     const int row = tr0 + r, col0 = tc0 + c8;
     if (row < s.rows && col0 < s.cols) {
       const int64_t e = shadow_pos(s.sfrag, s.cols, row, col0);
