@@ -258,8 +258,9 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 
 // ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
 constexpr int FC1_KB = 9;   // k-steps per load batch (288 k-steps = 32 batches)
+constexpr int FC1_AROW = FC1_KB * 32 * 2 + 16;   // LDS bytes per staged pool row (padded)
 
-__global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ pool,
+__global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
                                                       float* __restrict__ part, int B, int kchunk) {
   // XCD-aware mapping of the 1-D grid: workgroup w runs on XCD w % 8.  When the split
@@ -281,10 +282,11 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rl = lane & 15, kg = (lane >> 4) * 8;
   const int n0 = wave * 32;
-  // rows past B read row B-1 (valid data); their outputs are never stored
-  const int r0 = min(b0 + rl, B - 1), r1 = min(b0 + 16 + rl, B - 1);
-  const bf16* pa0 = pool + (int64_t)r0 * FEAT + kbeg + kg;
-  const bf16* pa1 = pool + (int64_t)r1 * FEAT + kbeg + kg;
+  // The pool tile (32 rows x 288 k per batch) is staged once per workgroup through LDS by
+  // whole-line loads (it was read by each of the 4 waves, as 16 half lines per load);
+  // rows are padded to 592 B, so the A-fragment reads (16 rows x 16 B per lane group) are
+  // bank-conflict-free.  Rows past B read row B-1 (valid data, outputs never stored).
+  __shared__ __attribute__((aligned(16))) char at[32 * FC1_AROW];
   // W1 is fragment-major (kernels.h frag_pos): the 16 x 32 fragment (n-tile, k-step) is
   // one 1-KB block and this lane's 16 B sit at lane * 8 in it
   const bf16* pb0 = wf1 + ((int64_t)((n0 >> 4) * (FEAT / 32) + (kbeg >> 5)) * 64 + lane) * 8;
@@ -294,18 +296,38 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int ACH = 32 * FC1_KB * 32 * 2 / 16;   // 16-B chunks of the A tile (1152)
   // K in batches of FC1_KB steps: every operand load of a batch is issued before its
   // MFMAs (kchunk is a multiple of 32 * FC1_KB: split factors divide 32)
   for (int kb = 0; kb < kchunk; kb += 32 * FC1_KB) {
-    bf16x8 a0[FC1_KB], a1[FC1_KB], w0[FC1_KB], w1[FC1_KB];
+    uint4 av[(ACH + 255) / 256];
+#pragma unroll
+    for (int u = 0; u < (ACH + 255) / 256; ++u) {
+      const int c = min((int)threadIdx.x + 256 * u, ACH - 1);   // clamped: rewrites the last
+      const int row = c / (FC1_KB * 4), col = c - row * (FC1_KB * 4);
+      av[u] = *reinterpret_cast<const uint4*>(pool + (int64_t)min(b0 + row, B - 1) * FEAT + kbeg +
+                                              kb + col * 8);
+    }
+    bf16x8 w0[FC1_KB], w1[FC1_KB];
 #pragma unroll
     for (int i = 0; i < FC1_KB; ++i) {
-      a0[i] = *reinterpret_cast<const bf16x8*>(pa0 + kb + 32 * i);
-      a1[i] = *reinterpret_cast<const bf16x8*>(pa1 + kb + 32 * i);
       w0[i] = *reinterpret_cast<const bf16x8*>(pb0 + (kb / 32 + i) * 512);
       w1[i] = *reinterpret_cast<const bf16x8*>(pb1 + (kb / 32 + i) * 512);
     }
-    __builtin_amdgcn_sched_barrier(0);   // all loads of the batch before its MFMAs
+    __builtin_amdgcn_sched_barrier(0);   // all loads of the batch before the staging
+#pragma unroll
+    for (int u = 0; u < (ACH + 255) / 256; ++u) {
+      const int c = min((int)threadIdx.x + 256 * u, ACH - 1);
+      const int row = c / (FC1_KB * 4), col = c - row * (FC1_KB * 4);
+      *reinterpret_cast<uint4*>(at + row * FC1_AROW + col * 16) = av[u];
+    }
+    __syncthreads();
+    bf16x8 a0[FC1_KB], a1[FC1_KB];
+#pragma unroll
+    for (int i = 0; i < FC1_KB; ++i) {
+      a0[i] = *reinterpret_cast<const bf16x8*>(at + rl * FC1_AROW + (32 * i + kg) * 2);
+      a1[i] = *reinterpret_cast<const bf16x8*>(at + (16 + rl) * FC1_AROW + (32 * i + kg) * 2);
+    }
 #pragma unroll
     for (int i = 0; i < FC1_KB; ++i) {
       acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w0[i], acc[0][0], 0, 0, 0);
@@ -313,6 +335,7 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ p
       acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w0[i], acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w1[i], acc[1][1], 0, 0, 0);
     }
+    __syncthreads();   // this batch's A reads are done before the next batch's staging
   }
   float* out = part + (int64_t)sidx * B * HID;
 #pragma unroll
