@@ -776,15 +776,13 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)   // waves 2,3: pair 4 is a discarded duplicate
-            // operands swapped (a1 fragment first): the accumulator is dW2^T, lane (g, i16)
-            // holding ci = 4g + r of co = i16, i.e. 4 consecutive slab floats (one 16-B store)
-            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bc[pi], Ac[mt], acc[pi][mt], 0, 0, 0);
+            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ac[mt], Bc[pi], acc[pi][mt], 0, 0, 0);
         }
       });
     };
     // the accumulators persist across the workgroup's images; after the last image they
-    // are stored while the dgrad waves are still computing.  acc[pi][mt] holds dW2^T:
-    // rows ci = 16nt + 4g + r, col co = 16mt + i16 (dW2[co][tap][ci] in the slab)
+    // are stored while the dgrad waves are still computing.  dW2[co][tap][ci]: rows
+    // co = 16mt + 4g + r, col ci = 16nt + i16
     auto per_image = [&](auto first, auto one, int i, bool last) __attribute__((always_inline)) {
       const int img = blockIdx.x * ipb + i;
       if (img < B) bwd_load_image<decltype(first)::value>(smem, img, xg, dpool, pmask, w1, b1, w2t, db2p);
@@ -806,10 +804,12 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           const int pair = wave + 4 * pi;
           const int tap = pair >> 1, nt = pair & 1;
           int o;   // laundered: 20 hoisted 64-bit store addresses would be spilled
-          asm volatile("v_mov_b32 %0, %1" : "=v"(o) : "v"(i16 * 288 + 4 * g));
+          asm volatile("v_mov_b32 %0, %1" : "=v"(o) : "v"(4 * g * 288 + i16));
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt)   // dW2[co = 16mt + i16][tap][ci = 16nt + 4g .. + 3]
-            *reinterpret_cast<f32x4*>(out + o + mt * 16 * 288 + tap * 32 + nt * 16) = acc[pi][mt];
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              out[o + (mt * 16 + r) * 288 + tap * 32 + nt * 16] = acc[pi][mt][r];
         }
         PDM_STAMP(3);
       }
