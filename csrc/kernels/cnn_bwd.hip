@@ -207,8 +207,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 
   if (bid < DW_TILES + nd) {
     // ---- dX tile: 32 batch rows x 384 features, K = 128 hidden ----
-    // Computed transposed, dpool^T[f][b] = W1^T[f][:] . dh^T[:][b]: the MFMA output lane then
-    // holds 4 consecutive features of one batch row, stored as one 8-byte bf16x4.  Each wave
+    // dpool[b][f] = dh[b][:] . W1^T[f][:] (A = dh, B = W1^T fragments): a lane holds 4 rows
+    // of one feature, so a wave's store covers 4 rows x 32 B.  (The transposed product with
+    // one 8-byte store per lane spread each store over 16 rows: 0.5 us slower.)  Each wave
     // owns 96 features (6 sub-tiles) x 32 rows with every operand load (24 W1^T + 8 dh
     // fragments) issued up front: at B = 256 the 192 tiles are one round of workgroups, each
     // a single load burst (the earlier 576 tiles of 128 features ran ~2.25 latency-bound
@@ -248,20 +249,20 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       for (int ft = 0; ft < DX_FT; ++ft)
 #pragma unroll
         for (int bt = 0; bt < 2; ++bt)
-          acc[ft][bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ft][ks], hb[bt][ks], acc[ft][bt], 0, 0, 0);
+          acc[ft][bt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hb[bt][ks], wa[ft][ks], acc[ft][bt], 0, 0, 0);
     FC_STAMP(t, 2);
+    // D[b][f]: lane (g, i16) holds rows b = 4g + r of feature i16: a store covers 4 rows x 32 B
 #pragma unroll
-    for (int bt = 0; bt < 2; ++bt) {
-      const int row = b0 + bt * 16 + i16;
-      if (row < B) {
+    for (int bt = 0; bt < 2; ++bt)
 #pragma unroll
-        for (int ft = 0; ft < DX_FT; ++ft) {
-          const bf16x4 o = {to_bf16(acc[ft][bt][0]), to_bf16(acc[ft][bt][1]),
-                            to_bf16(acc[ft][bt][2]), to_bf16(acc[ft][bt][3])};
-          *reinterpret_cast<bf16x4*>(dpool + (int64_t)row * FEAT + f0 + ft * 16 + 4 * g) = o;
+      for (int r = 0; r < 4; ++r) {
+        const int row = b0 + bt * 16 + 4 * g + r;
+        if (row < B) {
+#pragma unroll
+          for (int ft = 0; ft < DX_FT; ++ft)
+            dpool[(int64_t)row * FEAT + f0 + ft * 16 + i16] = to_bf16(acc[ft][bt][r]);
         }
       }
-    }
     FC_STAMP(t, 3);
     return;
   }
