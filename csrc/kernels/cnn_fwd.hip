@@ -210,7 +210,12 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx)
       aoff[ky * 3 + kx] = lp + (ky * H1 + kx) * 64 + ((g ^ ((2 * q + (s & 1) + kx) & 3)) << 4);
-  for (int tt = wave >> 1; tt < 36; tt += FWD_THREADS / 128) {
+  // wave pairs (w >> 1) 0, 1 take 10 tiles each, pairs 2, 3 take 8: a SIMD hosts waves w and
+  // w + 4, and the issue arbiter favours the older one, so with 9 tiles each waves 4-7
+  // finished ~1.3k cycles after waves 0-3, alone on their SIMDs
+  const int pr = wave >> 1;
+  const int tt0 = pr < 2 ? 10 * pr : 20 + 8 * (pr - 2), tt1 = tt0 + (pr < 2 ? 10 : 8);
+  for (int tt = tt0; tt < tt1; ++tt) {
     const int py = tt / 3, px0 = 4 * (tt - py * 3);
     const char* tb = a1s + (2 * py * H1 + 2 * px0) * 64;
     bf16x8 a[9];
@@ -242,6 +247,9 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     }
   }
   PDM_STAMP(3);
+  // per-wave conv2 end (waves 1-6 -> slots 10-15; blocks >= 64 only: the head overwrites
+  // slots 10-15 of blocks 0-63)
+  if ((threadIdx.x & 63) == 0 && wave >= 1 && wave <= 6) PDM_STAMP_VAL(9 + wave, PDM_CLOCK());
   __syncthreads();
   PDM_STAMP(4);
 

@@ -38,6 +38,11 @@ for which, names in (("fwd", ["start", "gathered(barrier)", "conv1(barrier)", "c
         hm = (hs - hb).median(dim=0).values
         print("   head: partials summed / xent / dh stored / slab acc / end (rel, median):",
               " ".join(f"{v:.0f}" for v in hm[1:].tolist()))
+    if which == "fwd" and B > 64:
+        ws = st[64:min(B, 256), 10:16] - st[64:min(B, 256), 0:1]
+        print("   conv2 end per wave 1..6 (rel, median):",
+              " ".join(f"{v:.0f}" for v in ws.median(dim=0).values.tolist()),
+              " wave 0:", f"{(st[64:min(B, 256), 3] - st[64:min(B, 256), 0]).median().item():.0f}")
     if which == "fwd":
         print("   image load issued (rel)", (st[:, 8] - st[:, 0]).median().item(),
               " image landed (rel)", (st[:, 9] - st[:, 0]).median().item())
