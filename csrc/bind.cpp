@@ -74,37 +74,59 @@ void check_data(const at::Tensor& images, const at::Tensor& labels, const at::Te
 }
 
 // ------------------------------------------------------------------ linear
-void lin_train(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tensor ctr, int64_t bfull,
-               int64_t B, at::Tensor W, at::Tensor b, at::Tensor slab) {
+// idx None: epoch-buffer mode, the step's rows are images[ctr*bfull + i] (the host keeps ctr
+// within the buffer); otherwise the sampler gather images[idx[ctr*bfull + i]].
+void lin_train(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx, at::Tensor ctr,
+               int64_t bfull, int64_t B, at::Tensor W, at::Tensor b, at::Tensor slab,
+               c10::optional<at::Tensor> metrics, c10::optional<at::Tensor> c1) {
   c10::DeviceGuard g(images.device());
-  check_data(images, labels, idx, ctr, bfull, B);
+  const bool gather = idx.has_value() && idx->defined();
+  int64_t nrow;
+  if (gather) {
+    check_data(images, labels, *idx, ctr, bfull, B);
+    nrow = idx->numel();
+  } else {
+    need(images, at::kByte, "images");
+    need(labels, at::kInt, "labels");
+    need(ctr, at::kLong, "ctr");
+    TORCH_CHECK(images.dim() == 2 && images.size(1) == 784 && images.size(0) >= B,
+                "images must be [>=B, 784]");
+    TORCH_CHECK(labels.numel() == images.size(0), "labels must be [N]");
+    TORCH_CHECK(B >= 1 && B <= bfull, "batch ", B, " must be in [1, ", bfull, "]");
+    nrow = images.size(0);
+  }
+  need_aligned(images.data_ptr(), 16, "images");        // 16-B row pieces (784 = 49 x 16)
   need(W, at::kFloat, "W");
   need(b, at::kFloat, "b");
   need(slab, at::kFloat, "slab");
   TORCH_CHECK(W.numel() == LIN_N * LIN_K && b.numel() == LIN_N, "W/b must be [10,784]/[10]");
+  need_aligned(W.data_ptr(), 16, "W");                  // float4 weight loads
   const int64_t nblk = (B + LIN_ROWS - 1) / LIN_ROWS;
   need_numel(slab, nblk * LIN_SLAB, "slab");
   need_aligned(slab.data_ptr(), 16, "slab");
-  launch_lin_train(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
-                   idx.numel(), ctr.data_ptr<int64_t>(), (int)bfull, (int)B, W.data_ptr<float>(),
-                   b.data_ptr<float>(), slab.data_ptr<float>(), cur_stream(images));
+  double* mp = nullptr;
+  if (metrics.has_value() && metrics->defined()) {
+    need(*metrics, at::kDouble, "metrics");
+    need_numel(*metrics, 3, "metrics");
+    mp = metrics->data_ptr<double>();
+  }
+  launch_lin_train(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
+                   gather ? idx->data_ptr<int32_t>() : nullptr, nrow, ctr.data_ptr<int64_t>(),
+                   (int)bfull, (int)B, W.data_ptr<float>(), b.data_ptr<float>(),
+                   slab.data_ptr<float>(), mp, opt_i64(c1), cur_stream(images));
 }
 
-void lin_reduce(at::Tensor slab, int64_t B, at::Tensor gW, at::Tensor gb, at::Tensor metrics,
-                c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1,
-                c10::optional<at::Tensor> xg) {
+void lin_reduce(at::Tensor slab, int64_t B, at::Tensor gW, at::Tensor gb,
+                c10::optional<at::Tensor> c0, c10::optional<at::Tensor> xg) {
   c10::DeviceGuard g(slab.device());
   need(slab, at::kFloat, "slab");
   need(gW, at::kFloat, "gW");
   need(gb, at::kFloat, "gb");
-  need(metrics, at::kDouble, "metrics");
   const int64_t nblk = (B + LIN_ROWS - 1) / LIN_ROWS;
   need_numel(slab, nblk * LIN_SLAB, "slab");
   TORCH_CHECK(gW.numel() == LIN_N * LIN_K && gb.numel() == LIN_N, "bad grad views");
-  need_numel(metrics, 3, "metrics");
   launch_lin_reduce(slab.data_ptr<float>(), (int)nblk, gW.data_ptr<float>(), gb.data_ptr<float>(),
-                    metrics.data_ptr<double>(), (int)B, opt_i64(c0), opt_i64(c1),
-                    xg_step(xg), cur_stream(slab));
+                    opt_i64(c0), xg_step(xg), cur_stream(slab));
 }
 
 void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
@@ -119,7 +141,8 @@ void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
   TORCH_CHECK(labels.numel() == images.size(0), "labels must be [N]");
   TORCH_CHECK(W.numel() == LIN_N * LIN_K && b.numel() == LIN_N, "W/b must be [10,784]/[10]");
   need_numel(metrics, 3, "metrics");
-  need_aligned(images.data_ptr(), 4, "images");
+  need_aligned(images.data_ptr(), 16, "images");
+  need_aligned(W.data_ptr(), 16, "W");
   if (images.size(0) == 0) return;
   launch_lin_eval(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), (int)images.size(0),
                   W.data_ptr<float>(), b.data_ptr<float>(), metrics.data_ptr<double>(),
@@ -154,7 +177,7 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd,
                 double momentum, double dampening, bool nesterov, double grad_scale,
                 std::vector<py::tuple> segs, c10::optional<at::Tensor> xg, int64_t signal_ch,
-                std::vector<int64_t> waits, double timeout_s) {
+                std::vector<int64_t> waits, double timeout_s, c10::optional<at::Tensor> bump) {
   c10::DeviceGuard dg(p.device());
   need(p, at::kFloat, "params");
   need(g, at::kFloat, "grads");
@@ -221,8 +244,9 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
       s.slab_col0 = (int32_t)sl[2].cast<int64_t>();
       s.slab_stride = sl[3].cast<int64_t>();
       const int64_t numel = (int64_t)s.rows * s.cols;
-      TORCH_CHECK(s.nslab >= 1 && numel % 4 == 0 && s.slab_col0 % 4 == 0 && s.slab_stride % 4 == 0 &&
-                      s.slab_col0 + numel <= s.slab_stride &&
+      // the reduction reads whole float4 groups: the slab row must hold the last group
+      TORCH_CHECK(s.nslab >= 1 && numel >= 4 && s.slab_col0 % 4 == 0 && s.slab_stride % 4 == 0 &&
+                      s.slab_col0 + ((numel + 3) / 4) * 4 <= s.slab_stride &&
                       st.numel() >= (int64_t)s.nslab * s.slab_stride, "gradient slab geometry");
       need_aligned(st.data_ptr(), 16, "gradient slab");
       s.slab = st.data_ptr<float>();
@@ -260,6 +284,7 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
   a.xg = opt_sync(xg);
   a.xg_signal_ch = (int)signal_ch;
   a.xg_timeout = (long long)(timeout_s * 1e8);
+  a.bump = opt_i64(bump);
   TORCH_CHECK(signal_ch >= -1 && signal_ch < XG_MAX_CH, "bad signal channel");
   TORCH_CHECK(a.xg != nullptr || (signal_ch < 0 && waits.empty()),
               "optimizer waits / signals need the xgmi sync words");
@@ -526,16 +551,18 @@ PYBIND11_MODULE(_C, m) {
   m.attr("XG_LOC_STEP") = XG_LOC_STEP;
   m.attr("XG_LOC_READY") = XG_LOC_READY;
   m.attr("XG_LOC_DONE") = XG_LOC_DONE;
-  m.def("lin_train", &lin_train);
+  m.def("lin_train", &lin_train, py::arg("images"), py::arg("labels"), py::arg("idx"),
+        py::arg("ctr"), py::arg("bfull"), py::arg("B"), py::arg("W"), py::arg("b"), py::arg("slab"),
+        py::arg("metrics") = py::none(), py::arg("c1") = py::none());
   m.def("lin_reduce", &lin_reduce, py::arg("slab"), py::arg("B"), py::arg("gW"), py::arg("gb"),
-        py::arg("metrics"), py::arg("c0"), py::arg("c1"), py::arg("xg") = py::none());
+        py::arg("c0") = py::none(), py::arg("xg") = py::none());
   m.def("lin_eval", &lin_eval);
   m.def("optim_step", &optim_step, py::arg("kind"), py::arg("p"), py::arg("g"), py::arg("m"),
         py::arg("v"), py::arg("lr"), py::arg("step"), py::arg("beta1"), py::arg("beta2"),
         py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"),
         py::arg("nesterov"), py::arg("grad_scale"), py::arg("segs"), py::arg("xg") = py::none(),
         py::arg("signal_ch") = -1, py::arg("waits") = std::vector<int64_t>{},
-        py::arg("timeout_s") = 60.0);
+        py::arg("timeout_s") = 60.0, py::arg("bump") = py::none());
   m.def("gather_epoch", &gather_epoch);
   m.def("xgmi_wait", &xgmi_wait);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;

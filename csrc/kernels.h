@@ -8,14 +8,21 @@
 // ---------------------------------------------------------------- linear model
 constexpr int LIN_K = 784;
 constexpr int LIN_N = 10;
-constexpr int LIN_ROWS = 8;
+#ifndef PDM_LIN_ROWS
+#define PDM_LIN_ROWS 4   // train rows per workgroup (4: 12.4 us/step; 8: 13.7; 16: 17.1 at B = 256)
+#endif
+constexpr int LIN_ROWS = PDM_LIN_ROWS;
 constexpr int LIN_SLAB = 7856;  // 7840 dW + 10 db + loss + correct, padded
+constexpr int LIN_EVAL_ROWS = 16;
 
+// idx == nullptr: rows [ctr*bfull, ctr*bfull + B) of `images` (epoch buffer), else the
+// sampler gather images[idx[ctr*bfull + i]].  metrics (fp64 [3]) and c1 (optimizer-step
+// counter, advanced once) are optional.
 void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                       int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W, const float* b,
-                      float* slab, hipStream_t st);
-void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, double* metrics, int B,
-                       int64_t* c0, int64_t* c1, unsigned* c2, hipStream_t st);
+                      float* slab, double* metrics, int64_t* c1, hipStream_t st);
+void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, int64_t* c0, unsigned* c2,
+                       hipStream_t st);
 void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, const float* W,
                      const float* b, double* metrics, hipStream_t st);
 
@@ -88,6 +95,9 @@ struct OptArgs {
   unsigned* xg;
   int xg_signal_ch;
   long long xg_timeout;   // s_memrealtime ticks
+  // optional counter advanced once by the launch (world size 1 Linear: the data-step
+  // counter, which no optimizer workgroup reads)
+  int64_t* bump;
 };
 
 void launch_optim(int kind, OptArgs& a, hipStream_t st);

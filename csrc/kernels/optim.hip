@@ -34,6 +34,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     if ((int)blockIdx.x >= a.seg[i].first_block) si = i;
   const OptSeg& s = a.seg[si];
   const int lb = blockIdx.x - s.first_block;
+  if (a.bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.bump += 1;
   if (a.xg != nullptr) {
     // xgmi streamed mode: publish the last bucket (every workgroup stores the same value,
     // so none depends on another being dispatched), then wait for this segment's bucket
@@ -82,7 +83,6 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     }
     return;
   }
-  const Hyper h = make_hyper<KIND>(a);
   float* __restrict__ P = a.p + s.offset;
   const float* __restrict__ G = a.g + s.offset;
   float* __restrict__ M = a.m + s.offset;
@@ -96,9 +96,20 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     __shared__ float4 red[16][16];
     const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
     const int e0 = lb * 64;
-    const int col = s.slab_col0 + min(e0 + 4 * c4, (int)numel - 4);   // clamped: stays in row
+    // clamped to the segment's last float4 group (the slab row holds the whole group)
+    const int col = s.slab_col0 + min(e0 + 4 * c4, (((int)numel + 3) & ~3) - 4);
     const float4* sp = reinterpret_cast<const float4*>(s.slab + col);
     const int64_t st4 = s.slab_stride / 4;
+    // the update's operands are loaded ahead of the slab reduction (one memory round trip
+    // fewer on the launch's critical path); the hyper-parameters are derived under the loads
+    const int e = e0 + tid;
+    const int ec = min(e, (int)numel - 1);
+    float p0 = 0.f, m0 = 0.f, v0 = 0.f;
+    if (tid < 64) {
+      p0 = P[ec];
+      m0 = M[ec];
+      if (KIND == OPT_ADAM) v0 = V[ec];
+    }
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int j0 = rg; j0 < s.nslab; j0 += 16 * 8) {
       float4 v[8];
@@ -115,17 +126,17 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       }
     }
     red[rg][c4] = acc;
+    const Hyper h = make_hyper<KIND>(a);
     __syncthreads();
-    const int e = e0 + tid;
     if (tid < 64 && e < numel) {
-      // numel % 4 == 0, so a valid element's float4 group is never a clamped one
+      // a valid element's float4 group is never a clamped one
       const float* rf = reinterpret_cast<const float*>(&red[0][0]);
       float gsum = 0.f;
 #pragma unroll
       for (int gq = 0; gq < 16; ++gq) gsum += rf[gq * 64 + tid];
       const_cast<float*>(G)[e] = gsum;              // the reduced gradient stays observable
-      float m = M[e], v = (KIND == OPT_ADAM) ? V[e] : 0.f;
-      const float p = update<KIND>(P[e], gsum, m, v, h, a.grad_scale);
+      float m = m0, v = v0;
+      const float p = update<KIND>(p0, gsum, m, v, h, a.grad_scale);
       P[e] = p;
       M[e] = m;
       if (KIND == OPT_ADAM) V[e] = v;
@@ -136,6 +147,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     return;
   }
 
+  const Hyper h = make_hyper<KIND>(a);
   if (s.shadow_t == nullptr) {
     // plain segment: 8 contiguous floats per thread (2 x float4)
     const int64_t e0 = (int64_t)lb * CHUNK + threadIdx.x * 8;

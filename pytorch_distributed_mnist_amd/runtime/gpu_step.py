@@ -6,11 +6,12 @@ inputs (batch indices come from a device step counter), so it is captured once
 per batch size into a ``torch.cuda.CUDAGraph`` (hipGraph) and replayed.
 
 Counter protocol (kernels of one step must not race on a counter): the first
-kernel reads the data-step counter; a *middle* kernel (``lin_reduce`` /
-``cnn_head``) advances both the data-step and the optimizer-step counters; the
-optimizer kernel reads the already-advanced optimizer step (t >= 1).
+kernel reads the data-step counter and only a later kernel advances it; the
+optimizer-step counter is advanced before the optimizer kernel reads it (t >= 1).
+CNN: ``cnn_head`` advances both.  Linear: ``lin_train`` advances the optimizer
+step, ``lin_reduce`` (or, at world size 1, the optimizer launch) the data step.
 
-Linear (reference Net, fp32):  lin_train -> lin_reduce -> [all-reduce] -> optim
+Linear (reference Net, fp32):  lin_train -> [lin_reduce -> all-reduce] -> optim
 CNN (bf16):  cnn_fwd -> fc1_fwd -> cnn_head -> fc1_bwd -> [all-reduce bucket 0]
              -> cnn_bwd -> conv_reduce -> [all-reduce bucket 1] -> optim
 """
@@ -162,7 +163,7 @@ class GpuStepBase:
         """[(offset, rows, cols, shadow|None, shadow_t|None)] covering the arena."""
         return [(0, 1, self.arena.spec.total, None, None)]
 
-    def launch_optimizer(self, segments=None, signal_ch: int = -1) -> None:
+    def launch_optimizer(self, segments=None, signal_ch: int = -1, bump=None) -> None:
         """One fused optimizer launch over `segments` (default: every parameter).
 
         xgmi streamed mode: bucket `signal_ch` (>= 0) is published to the persistent
@@ -195,13 +196,13 @@ class GpuStepBase:
             self.C.optim_step(self.C.OPT_ADAM, self.arena.params, grads, o.exp_avg,
                               o.exp_avg_sq, o._lr_dev, o._step_dev, float(b1), float(b2),
                               float(g["eps"]), float(g["weight_decay"]), 0.0, 0.0, False,
-                              float(self.reducer.grad_scale), segs, **xg)
+                              float(self.reducer.grad_scale), segs, bump=bump, **xg)
         else:
             self.C.optim_step(self.C.OPT_SGD, self.arena.params, grads,
                               o.momentum_buffer, None, o._lr_dev, o._step_dev, 0.0, 0.0, 0.0,
                               float(g["weight_decay"]), float(g["momentum"]),
                               float(g["dampening"]), bool(g["nesterov"]),
-                              float(self.reducer.grad_scale), segs, **xg)
+                              float(self.reducer.grad_scale), segs, bump=bump, **xg)
 
     def invalidate_graphs(self) -> None:
         self.graphs.clear()
@@ -209,6 +210,10 @@ class GpuStepBase:
 
 
 class LinearStep(GpuStepBase):
+    """Reference Net step.  world size 1: lin_train -> optim (the optimizer sums the
+    per-workgroup gradient slabs itself and advances the data-step counter);
+    world size > 1: lin_train -> lin_reduce -> [all-reduce] -> optim."""
+
     def __init__(self, prog, use_graphs):
         super().__init__(prog, use_graphs)
         nblk = (self.bfull + self.C.LIN_ROWS - 1) // self.C.LIN_ROWS
@@ -217,14 +222,51 @@ class LinearStep(GpuStepBase):
         self.b = self.arena.param("fc.bias")
         self.gW = self.arena.grad("fc.weight")
         self.gb = self.arena.grad("fc.bias")
+        # world size 1 (no all-reduce between backward and update): the slab reduction runs
+        # inside the optimizer launch (PDM_FUSE_LIN_REDUCE=0 disables)
+        self.fuse_reduce = (not self.reducer.active and
+                            os.environ.get("PDM_FUSE_LIN_REDUCE", "1") != "0")
+        self._fused = {}
+        self.ep_images = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.ep_labels = torch.empty(0, dtype=torch.int32, device=self.device)
+
+    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
+        """Upload the epoch order, then materialise the epoch's samples contiguously (the
+        step kernel then reads its rows behind one counter load instead of two)."""
+        n = idx_cpu.numel()
+        if self.ep_images.numel() != n * 784:
+            self.ep_images = torch.empty(n * 784, dtype=torch.uint8, device=self.device)
+            self.ep_labels = torch.empty(n, dtype=torch.int32, device=self.device)
+            self.graphs.clear()
+        super().set_train_indices(idx_cpu)
+        self.C.gather_epoch(self.train_images, self.train_labels, self.idx,
+                            self.ep_images.view(n, 784), self.ep_labels)
+
+    def invalidate_graphs(self) -> None:
+        super().invalidate_graphs()
+        self._fused = {}
+
+    def _fused_segments(self, nblk: int):
+        segs = self._fused.get(nblk)
+        if segs is None:
+            C, spec = self.C, self.arena.spec
+            sl = lambda col: (self.slab, nblk, col, C.LIN_SLAB)
+            segs = [(spec.offset("fc.weight"), 10, 784, None, None, sl(0)),
+                    (spec.offset("fc.bias"), 1, 10, None, None, sl(7840))]
+            self._fused[nblk] = segs
+        return segs
 
     def _train_impl(self, B: int) -> None:
         C = self.C
-        C.lin_train(self.train_images, self.train_labels, self.idx, self.ctr[0:1], self.bfull, B,
-                    self.W, self.b, self.slab)
+        C.lin_train(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull,
+                    B, self.W, self.b, self.slab, self.metrics.train_view(), self.opt._step_dev)
         red = self.reducer
-        C.lin_reduce(self.slab, B, self.gW, self.gb, self.metrics.train_view(), self.ctr[0:1],
-                     self.opt._step_dev, red.sync if red.streamed else None)
+        if self.fuse_reduce:
+            nblk = (B + C.LIN_ROWS - 1) // C.LIN_ROWS
+            self.launch_optimizer(self._fused_segments(nblk), bump=self.ctr[0:1])
+            return
+        C.lin_reduce(self.slab, B, self.gW, self.gb, self.ctr[0:1],
+                     red.sync if red.streamed else None)
         if red.streamed:
             # the optimizer publishes the bucket and waits for the persistent collective
             self.launch_optimizer(signal_ch=0)

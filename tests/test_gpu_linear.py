@@ -10,8 +10,9 @@ from pytorch_distributed_mnist_amd.runtime.program import build_local_program
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("gather", [True, False])
 @pytest.mark.parametrize("B,bfull", [(256, 256), (96, 256), (1, 8), (13, 32)])
-def test_lin_train_reduce_matches_torch(gpu, B, bfull):
+def test_lin_train_reduce_matches_torch(gpu, B, bfull, gather):
     from pytorch_distributed_mnist_amd.ops import _ext
     C = _ext.require()
     g = torch.Generator().manual_seed(B)
@@ -38,9 +39,13 @@ def test_lin_train_reduce_matches_torch(gpu, B, bfull):
     metrics = torch.zeros(3, dtype=torch.float64, device=dev)
     gW = torch.zeros(10, 784, device=dev)
     gb = torch.zeros(10, device=dev)
-    C.lin_train(images.to(dev), labels.to(dev, torch.int32), idx.to(dev), ctr[0:1], bfull, B,
-                W.to(dev), b.to(dev), slab)
-    C.lin_reduce(slab, B, gW, gb, metrics, ctr[0:1], ostep)
+    if gather:        # sampler gather: images[idx[ctr * bfull + i]]
+        C.lin_train(images.to(dev), labels.to(dev, torch.int32), idx.to(dev), ctr[0:1], bfull, B,
+                    W.to(dev), b.to(dev), slab, metrics, ostep)
+    else:             # epoch buffer: rows ctr * bfull + i of the gathered epoch
+        C.lin_train(images[idx.long()].to(dev), labels[idx.long()].to(dev, torch.int32), None,
+                    ctr[0:1], bfull, B, W.to(dev), b.to(dev), slab, metrics, ostep)
+    C.lin_reduce(slab, B, gW, gb, ctr[0:1])
     torch.cuda.synchronize()
     assert torch.allclose(gW.cpu(), Wr.grad, atol=2e-6, rtol=1e-4)
     assert torch.allclose(gb.cpu(), br.grad, atol=2e-6, rtol=1e-4)
@@ -84,6 +89,7 @@ def test_linear_epoch_gpu_matches_cpu(gpu, graphs, opt):
         el, ea = p.evaluate()
         progs[dev] = (p, tl, ta, el, ea)
     pc, pg = progs["cpu"][0], progs["cuda"][0]
+    assert pg.gpu.fuse_reduce            # world size 1: slab reduction inside the optimizer
     assert pg.steps_per_epoch == 9    # ragged tail of 96 included
     diff = (pc.arena.params - pg.arena.params.cpu()).abs().max().item()
     assert diff < 5e-5, diff
@@ -91,3 +97,26 @@ def test_linear_epoch_gpu_matches_cpu(gpu, graphs, opt):
     assert progs["cpu"][2].correct == progs["cuda"][2].correct
     assert abs(progs["cpu"][3].average - progs["cuda"][3].average) < 1e-4
     assert pg.optimizer.step_count == 9 and int(pg.optimizer._step_dev.item()) == 9
+
+
+@pytest.mark.parametrize("opt", ["adam", "sgd"])
+def test_linear_fused_reduce_matches_unfused(gpu, opt, monkeypatch):
+    """World size 1 sums the gradient slabs inside the optimizer launch; the unfused chain
+    (lin_reduce -> optim, the multi-GPU structure) must give the same training run."""
+    train = synthetic_split(1024 + 40, True)
+    test = synthetic_split(256, False)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("PDM_FUSE_LIN_REDUCE", fuse)
+        p = build_local_program("linear", "fp32", "cuda", 128, train, test, optimizer=opt,
+                                lr=1e-3 if opt == "adam" else 0.05, seed=3, use_graphs=True)
+        assert p.gpu.fuse_reduce == (fuse == "1")
+        p.optimizer.sync_hyperparams()
+        p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        tl, ta = p.train_epoch()
+        out[fuse] = (p.arena.params.clone(), tl.average, ta.correct, p.gpu.ctr[0].item(),
+                     int(p.optimizer._step_dev.item()))
+    a, b = out["1"], out["0"]
+    assert (a[0] - b[0]).abs().max().item() < 1e-6
+    assert abs(a[1] - b[1]) < 1e-9 and a[2] == b[2]
+    assert a[3] == b[3] == 9 and a[4] == b[4] == 9
