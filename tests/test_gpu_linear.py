@@ -118,5 +118,5 @@ def test_linear_fused_reduce_matches_unfused(gpu, opt, monkeypatch):
                      int(p.optimizer._step_dev.item()))
     a, b = out["1"], out["0"]
     assert (a[0] - b[0]).abs().max().item() < 1e-6
-    assert abs(a[1] - b[1]) < 1e-9 and a[2] == b[2]
+    assert abs(a[1] - b[1]) < 1e-6 and a[2] == b[2]   # slab sums in a different order
     assert a[3] == b[3] == 9 and a[4] == b[4] == 9
