@@ -32,6 +32,25 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Whole-wave sum on the DPP network, no LDS traffic: quad swaps and row rotates leave every
+// lane of a 16-lane row with the row's sum, then the four row sums are read as scalars.
+// The result is identical in every lane (a different addition order than wave_sum).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x124>(v);   // row_ror:4
+  v += dpp_mov<0x128>(v);   // row_ror:8
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // Sum within aligned groups of `width` lanes (width a power of two <= 64).
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
 
     float lg[NCLS];
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) lg[c] = wave_sum(fmaf(h.y, w2v[c].y, h.x * w2v[c].x)) + bf2[c];
+    for (int c = 0; c < NCLS; ++c) lg[c] = wave_sum_dpp(fmaf(h.y, w2v[c].y, h.x * w2v[c].x)) + bf2[c];
     float prob[NCLS];
     int correct;
     const float loss = row_xent<NCLS>(lg, y, prob, correct);

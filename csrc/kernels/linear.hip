@@ -92,7 +92,7 @@ __device__ __forceinline__ void wave_logits(const float (*xs)[K], const int (&ro
 #pragma unroll
   for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int n = 0; n < N; ++n) lg[i][n] = wave_sum(acc[i][n]) + bias[n];
+    for (int n = 0; n < N; ++n) lg[i][n] = wave_sum_dpp(acc[i][n]) + bias[n];
 }
 
 // log-softmax CE on one row's logits; returns loss, writes softmax probs, sets
@@ -132,7 +132,10 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
   const int row0 = blockIdx.x * ROWS;
   const int nrows = min(ROWS, B - row0);
 
-  // 1. the step's rows: counter -> (sampler index ->) 16-B image loads, labels
+  // 1. weights into registers: issued first, so they travel under the counter -> image chain
+  float4 w[N][KJ];
+  load_w_regs(W, w);
+  // 2. the step's rows: counter -> (sampler index ->) 16-B image loads, labels
   const int64_t base = (*ctr) * (int64_t)bfull + row0;
   PDM_CHECK(base + nrows <= nrow, "lin_train sample row past the epoch", base, nrow);
   // row -> sample (clamped: a counter driven past the epoch reads a valid row, not a fault)
@@ -154,9 +157,7 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
       px[u] = reinterpret_cast<const uint4*>(images + sample(pr[u]) * K)[pq[u]];
   }
   if (tid < ROWS) lab[tid] = tid < nrows ? labels[sample(tid)] : 0;
-  // 2. weights into registers (in flight with the image), normalisation table
-  float4 w[N][KJ];
-  load_w_regs(W, w);
+  // normalisation table (built while the image is in flight)
   lut[tid] = pdm_normalize((uint32_t)tid);
   __syncthreads();
 #pragma unroll
