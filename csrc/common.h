@@ -51,6 +51,20 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   return (r0 + r1) + (r2 + r3);
 }
 
+// v + v[lane ^ 8], v[lane ^ 16], v[lane ^ 32] without LDS traffic: row_ror:8 is the xor-8
+// partner inside a 16-lane row; gfx950's permlane16/32 swaps exchange odd and even rows /
+// the two wave halves (both results summed in the same order as the shuffle butterfly).
+// Full EXEC required.
+__device__ __forceinline__ float sum_xor8(float v) { return v + dpp_mov<0x128>(v); }
+__device__ __forceinline__ float sum_xor16(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(a[0]) + __int_as_float(a[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(a[0]) + __int_as_float(a[1]);
+}
+
 // Sum within aligned groups of `width` lanes (width a power of two <= 64).
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {

@@ -876,13 +876,11 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) r1[(nt * 16 + 4 * g + r) * 16 + i16] += acc1[nt][r];
   }
-  // conv2 bias: lanes sharing (lane & 7) hold the same 8 channels
+  // conv2 bias: lanes sharing (lane & 7) hold the same 8 channels (DPP / permlane swaps:
+  // the shuffle butterfly's 24 LDS bpermutes each waited out a full LDS round trip)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    float v = db2p[j];
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
+    const float v = sum_xor32(sum_xor16(sum_xor8(db2p[j])));
     if (lane < 8) red[RED_DB2 + wave * C2 + lane * 8 + j] = v;
   }
   __syncthreads();
