@@ -97,6 +97,9 @@ def test_xgmi_two_ranks_one_gpu(gpu, tmp_path):
         # 2-rank sums are a + b on both transports: bit-identical training
         assert d["cnn_equal"], d
         assert d["replicas_equal"]
+        # the reference Net through the multi-GPU chain (lin_reduce, streamed collective)
+        assert d["lin_kinds"] == ["xgmi", "torch"]
+        assert d["lin_equal"] and d["lin_replicas_equal"], d
 
 
 def test_xgmi_four_ranks_one_gpu(gpu, tmp_path):
@@ -108,6 +111,7 @@ def test_xgmi_four_ranks_one_gpu(gpu, tmp_path):
         # above, the two trainings only have to stay close (bf16 weights amplify the
         # last-bit differences over 20 SGD steps)
         assert d["cnn_max_diff"] < 5e-2, d
+        assert d["lin_replicas_equal"] and d["lin_max_diff"] < 1e-3, d
 
 
 def test_xgmi_absent_peer_fails_fast(gpu, tmp_path):

@@ -82,7 +82,7 @@ def check_collective(comm, dev, rank, ws, mode):
     return bool(ok), [d["mode"] for d in desc]
 
 
-def train_cnn(comm, dev, rank, ws, transport):
+def train_model(arch, comm, dev, rank, ws, transport):
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.models.reference import MODULES
@@ -93,19 +93,22 @@ def train_cnn(comm, dev, rank, ws, transport):
     from pytorch_distributed_mnist_amd.runtime.program import TrainProgram
     os.environ["PDM_XGMI_MODE"] = "auto"
     torch.manual_seed(1234)
-    spec = get_spec("cnn")
+    spec = get_spec(arch)
     arena = FlatArena(spec, dev)
-    arena.load_module(MODULES["cnn"]())
-    opt = build_optimizer("sgd", arena, SimpleNamespace(lr=0.05, momentum=0.9, weight_decay=1e-4))
+    arena.load_module(MODULES[arch]())
+    cnn = arch == "cnn"
+    opt = build_optimizer("sgd" if cnn else "adam", arena,
+                          SimpleNamespace(lr=0.05 if cnn else 1e-3, momentum=0.9, weight_decay=1e-4))
     red = GradReducer(comm, arena.grads, spec.bucket_bounds(), transport=transport)
     train = synthetic_split(128 * ws * 9 + 40, True)
     test = synthetic_split(256, False)
-    prog = TrainProgram("cnn", "bf16", arena, opt, red, train, test, 128, use_graphs=True)
+    prog = TrainProgram(arch, "bf16" if cnn else "fp32", arena, opt, red, train, test, 128,
+                        use_graphs=True)
     opt.sync_hyperparams()
     for epoch in range(2):
         prog.set_train_indices(distributed_indices(len(train), ws, rank, epoch))
         prog.train_epoch()
-        log(f"cnn {transport}: epoch {epoch} done")
+        log(f"{arch} {transport}: epoch {epoch} done")
     torch.cuda.synchronize()
     red.check()
     kind = red.kind
@@ -215,8 +218,8 @@ def main():
         ok, modes = check_collective(comm, dev, rank, ws, mode)
         res[mode] = ok
         res[mode + "_modes"] = modes
-    p_x, kind_x = train_cnn(comm, dev, rank, ws, "xgmi")
-    p_g, kind_g = train_cnn(comm, dev, rank, ws, None)       # gloo data plane
+    p_x, kind_x = train_model("cnn", comm, dev, rank, ws, "xgmi")
+    p_g, kind_g = train_model("cnn", comm, dev, rank, ws, None)       # gloo data plane
     res["cnn_kinds"] = [kind_x, kind_g]
     res["cnn_max_diff"] = float((p_x - p_g).abs().max())
     res["cnn_equal"] = bool(torch.equal(p_x, p_g))
@@ -224,6 +227,15 @@ def main():
     parts = [torch.zeros_like(p_x.cpu()) for _ in range(ws)]
     dist.all_gather(parts, p_x.cpu())
     res["replicas_equal"] = all(torch.equal(parts[0], q) for q in parts[1:])
+    # the reference Net (Linear, fp32, Adam): lin_train -> lin_reduce -> all-reduce -> optim
+    l_x, lkind_x = train_model("linear", comm, dev, rank, ws, "xgmi")
+    l_g, lkind_g = train_model("linear", comm, dev, rank, ws, None)
+    res["lin_kinds"] = [lkind_x, lkind_g]
+    res["lin_max_diff"] = float((l_x - l_g).abs().max())
+    res["lin_equal"] = bool(torch.equal(l_x, l_g))
+    parts = [torch.zeros_like(l_x.cpu()) for _ in range(ws)]
+    dist.all_gather(parts, l_x.cpu())
+    res["lin_replicas_equal"] = all(torch.equal(parts[0], q) for q in parts[1:])
     with open(os.path.join(os.environ["PDM_XGMI_OUT"], f"rank{rank}.json"), "w") as f:
         json.dump(res, f)
     dist.destroy_process_group()
