@@ -76,6 +76,23 @@ __device__ __forceinline__ float group_sum(float v) {
 __device__ __forceinline__ bf16 to_bf16(float f) { return (bf16)f; }
 __device__ __forceinline__ float from_bf16(bf16 h) { return (float)h; }
 
+// Stores of per-workgroup gradient slabs (read once, by the next launch).  PDM_NT=1
+// (diagnostic builds): streaming (non-temporal) stores and loads for them.
+#ifndef PDM_NT
+#define PDM_NT 0
+#endif
+__device__ __forceinline__ void pdm_slab_store(float* p, float v) {
+  if (PDM_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ float4 pdm_slab_load4(const float4* p) {
+  if (PDM_NT) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  return *p;
+}
+
 // Bookkeeping done by exactly one thread of a kernel that no other kernel of the
 // same step reads concurrently (see runtime/gpu_step.py: the "middle" kernel
 // advances the data-step and optimizer-step counters).

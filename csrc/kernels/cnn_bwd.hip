@@ -810,7 +810,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              out[o + (mt * 16 + r) * 288 + tap * 32 + nt * 16] = acc[pi][mt][r];
+              pdm_slab_store(&out[o + (mt * 16 + r) * 288 + tap * 32 + nt * 16], acc[pi][mt][r]);
         }
         PDM_STAMP(3);
       }

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     for (int j0 = rg; j0 < s.nslab; j0 += 16 * 8) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)min(j0 + 16 * u, s.nslab - 1) * st4];
+      for (int u = 0; u < 8; ++u) v[u] = pdm_slab_load4(sp + (int64_t)min(j0 + 16 * u, s.nslab - 1) * st4);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {

@@ -66,7 +66,7 @@ def compile_flags(abi: int, inc):
         flags.append("-DPDM_DEBUG_BOUNDS=1")
     if os.environ.get("PDM_STAMPS"):
         flags.append("-DPDM_STAMPS=1")
-    for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS"):   # tuning experiments (diagnostic builds)
+    for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS", "PDM_NT"):   # tuning experiments (diagnostic builds)
         if os.environ.get(k):
             flags.append(f"-D{k}={int(os.environ[k])}")
     return flags
@@ -136,7 +136,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     keep = set(objs)
     variant = custom_out or any(os.environ.get(k) for k in
                                      ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL",
-                                      "PDM_LIN_ROWS"))
+                                      "PDM_LIN_ROWS", "PDM_NT"))
     for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not variant else []:
         if o not in keep:
             try:
