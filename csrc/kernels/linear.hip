@@ -26,9 +26,11 @@ namespace {
 
 constexpr int K = LIN_K;        // 784
 constexpr int N = LIN_N;        // 10
-constexpr int ROWS = LIN_ROWS;  // rows per block (train): 4, 8 or 16
-constexpr int RPW = ROWS / 4;   // rows per wave
-static_assert(ROWS % 4 == 0 && RPW <= 4, "LIN_ROWS must be 4, 8, 12 or 16");
+constexpr int ROWS = LIN_ROWS;  // rows per block (train): 2, 4, 8 or 16
+constexpr int NWV = ROWS < 4 ? ROWS : 4;     // waves per block
+constexpr int RPW = ROWS / NWV;              // rows per wave
+constexpr int THREADS = 64 * NWV;
+static_assert(ROWS % NWV == 0 && RPW <= 4, "LIN_ROWS must be 1, 2, 4, 8, 12 or 16");
 constexpr int K4 = K / 4;       // 196 float4 columns
 constexpr int KJ = 4;           // 256-feature chunks per row (the last holds 16 features)
 constexpr int Q16 = K / 16;     // 49 16-byte pieces per image row
@@ -118,7 +120,7 @@ __device__ __forceinline__ float row_xent(const float (&lg)[N], int y, float (&p
   return lse - ly;
 }
 
-__global__ __launch_bounds__(256) void lin_train_kernel(
+__global__ __launch_bounds__(THREADS) void lin_train_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
     int B, const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ slab,
@@ -144,12 +146,12 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
     return idx ? (int64_t)idx[i] : i;
   };
   constexpr int NPIECE = ROWS * Q16;                 // 16-B pieces of the block's rows
-  constexpr int PPT = (NPIECE + 255) / 256;          // per thread
+  constexpr int PPT = (NPIECE + THREADS - 1) / THREADS;   // per thread
   uint4 px[PPT];
   int pr[PPT], pq[PPT];
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {
-    const int i = tid + 256 * u;
+    const int i = tid + THREADS * u;
     pr[u] = i / Q16;
     pq[u] = i - pr[u] * Q16;
     px[u] = make_uint4(0u, 0u, 0u, 0u);
@@ -158,22 +160,23 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
   }
   if (tid < ROWS) lab[tid] = tid < nrows ? labels[sample(tid)] : 0;
   // normalisation table (built while the image is in flight)
-  lut[tid] = pdm_normalize((uint32_t)tid);
+#pragma unroll
+  for (int i = tid; i < 256; i += THREADS) lut[i] = pdm_normalize((uint32_t)i);
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
-    if (tid + 256 * u < NPIECE) put_pixels(xs[pr[u]], pq[u], px[u], lut);   // zeros past nrows
+    if (tid + THREADS * u < NPIECE) put_pixels(xs[pr[u]], pq[u], px[u], lut);   // zeros past nrows
   __syncthreads();
 
-  // 3. logits of rows wave + 4 i; lane i runs the CE of row wave + 4 i
+  // 3. logits of rows wave + NWV i; lane i runs the CE of row wave + NWV i
   {
     int rows[RPW];
 #pragma unroll
-    for (int i = 0; i < RPW; ++i) rows[i] = wave + 4 * i;
+    for (int i = 0; i < RPW; ++i) rows[i] = wave + NWV * i;
     float lg[RPW][N];
     wave_logits<RPW>(xs, rows, w, bias, lg);
     if (lane < RPW) {
-      const int r = wave + 4 * lane;
+      const int r = wave + NWV * lane;
       float l[N], p[N];
 #pragma unroll
       for (int n = 0; n < N; ++n) {
@@ -202,10 +205,10 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
 
   // 4. partial dW = dl^T x (thread -> 4 consecutive features), db, metrics
   float* out = slab + (int64_t)blockIdx.x * LIN_SLAB;
-  if (tid < K4) {
+  for (int c = tid; c < K4; c += THREADS) {
     float4 x[ROWS];
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r) x[r] = reinterpret_cast<const float4*>(xs[r])[tid];
+    for (int r = 0; r < ROWS; ++r) x[r] = reinterpret_cast<const float4*>(xs[r])[c];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -217,15 +220,18 @@ __global__ __launch_bounds__(256) void lin_train_kernel(
         s.z = fmaf(d, x[r].z, s.z);
         s.w = fmaf(d, x[r].w, s.w);
       }
-      reinterpret_cast<float4*>(out + n * K)[tid] = s;
+      reinterpret_cast<float4*>(out + n * K)[c] = s;
     }
-  } else if (tid < K4 + N) {
-    const int n = tid - K4;
+  }
+  // db and the metrics on threads past the last dW column when there are any
+  constexpr int TDB = THREADS > K4 + N ? K4 : THREADS - N - 1;
+  if (tid >= TDB && tid < TDB + N) {
+    const int n = tid - TDB;
     float s = 0.f;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) s += dl[r][n];
     out[N * K + n] = s;
-  } else if (tid == K4 + N) {
+  } else if (tid == TDB + N) {
     float l = 0.f, c = 0.f;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) { l += red[r][0]; c += red[r][1]; }
@@ -323,7 +329,7 @@ void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_
                       int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W,
                       const float* b, float* slab, double* metrics, int64_t* c1, hipStream_t st) {
   const int nblk = (B + ROWS - 1) / ROWS;
-  lin_train_kernel<<<nblk, 256, 0, st>>>(images, labels, idx, nrow, ctr, bfull, B, W, b, slab,
+  lin_train_kernel<<<nblk, THREADS, 0, st>>>(images, labels, idx, nrow, ctr, bfull, B, W, b, slab,
                                          metrics, c1);
 }
 
