@@ -69,6 +69,8 @@ def compile_flags(abi: int, inc):
     for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS", "PDM_NT"):   # tuning experiments (diagnostic builds)
         if os.environ.get(k):
             flags.append(f"-D{k}={int(os.environ[k])}")
+    if os.environ.get("PDM_HIPCC_FLAGS"):                  # compiler experiments (diagnostic builds)
+        flags += os.environ["PDM_HIPCC_FLAGS"].split()
     return flags
 
 
@@ -136,7 +138,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     keep = set(objs)
     variant = custom_out or any(os.environ.get(k) for k in
                                      ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL",
-                                      "PDM_LIN_ROWS", "PDM_NT"))
+                                      "PDM_LIN_ROWS", "PDM_NT", "PDM_HIPCC_FLAGS"))
     for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not variant else []:
         if o not in keep:
             try:
