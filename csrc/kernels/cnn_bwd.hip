@@ -27,6 +27,20 @@
 #include <type_traits>
 #include <utility>
 
+// Translation-unit split: fc1_bwd is compiled from fc1_bwd.hip (this file with
+// PDM_FC1_BWD_TU = 1) under its own scheduler flags (build.py FILE_FLAGS); this file's own
+// compile holds the rest.  PDM_STAMPS builds keep everything here (one stamp buffer).
+#ifndef PDM_FC1_BWD_TU
+#define PDM_FC1_BWD_TU 0
+#endif
+#if defined(PDM_STAMPS)
+#define PDM_WANT_FC1_BWD (PDM_FC1_BWD_TU == 0)
+#define PDM_WANT_REST (PDM_FC1_BWD_TU == 0)
+#else
+#define PDM_WANT_FC1_BWD (PDM_FC1_BWD_TU == 1)
+#define PDM_WANT_REST (PDM_FC1_BWD_TU == 0)
+#endif
+
 namespace {
 
 using namespace cnn;
@@ -41,6 +55,7 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+#if PDM_WANT_FC1_BWD
 // ------------------------------------------------------------------ fc1_bwd
 // diagnostic stamps (PDM_STAMPS builds; tools/stamps_fc.py): dX tile t -> row t, slots 0-3;
 // dW tile b -> row b, slots 8-13 (cnn_bwd overwrites them, so fc1_bwd is stamped alone)
@@ -302,6 +317,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     }
   }
 }
+
+#endif  // PDM_WANT_FC1_BWD
+#if PDM_WANT_REST
 
 // ------------------------------------------------------------------ cnn_bwd
 // LDS carve (one static array, 163,200 B -> 1 workgroup / CU):
@@ -946,8 +964,10 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
   }
 }
 
+#endif  // PDM_WANT_REST
 }  // namespace
 
+#if PDM_WANT_FC1_BWD
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
@@ -963,6 +983,8 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
                                        head_blocks, gwf2, gbf2, gbf1, metrics, off, fcu);
 }
 
+#endif
+#if PDM_WANT_REST
 int cnn_bwd_blocks(int B, int ipb) { return (B + ipb - 1) / ipb; }
 
 void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
@@ -990,3 +1012,4 @@ void read_stamps_bwd(unsigned long long* host) {
   for (int i = 0; i < 256 * 16; ++i) host[i] = 0;
 }
 #endif
+#endif  // PDM_WANT_REST

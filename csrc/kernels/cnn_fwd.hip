@@ -18,10 +18,24 @@
 //             fc1 weight-gradient GEMM), fc1 bias partials; advances step counters.
 #include "cnn_common.h"
 
+// Translation-unit split: fc1_fwd is compiled from fc1_fwd.hip (this file with
+// PDM_FC1_FWD_TU = 1) under its own scheduler flags (build.py FILE_FLAGS); this file's own
+// compile holds cnn_fwd and the head.  PDM_STAMPS builds keep everything here.
+#ifndef PDM_FC1_FWD_TU
+#define PDM_FC1_FWD_TU 0
+#endif
+#if defined(PDM_STAMPS)
+#define PDM_WANT_FC1_FWD (PDM_FC1_FWD_TU == 0)
+#else
+#define PDM_WANT_FC1_FWD (PDM_FC1_FWD_TU == 1)
+#endif
+#define PDM_WANT_FWD_REST (PDM_FC1_FWD_TU == 0)
+
 namespace {
 
 using namespace cnn;
 
+#if PDM_WANT_FWD_REST
 // ---- cnn_fwd LDS carve (one static array; every offset 16-B aligned) ----
 constexpr int FWD_THREADS = 512;
 constexpr int F_X3 = 0;                       // bf16x4 x3[p] = x[p..p+2], 0  6272 B
@@ -264,6 +278,8 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   PDM_STAMP(5);
 }
 
+#endif  // PDM_WANT_FWD_REST
+#if PDM_WANT_FC1_FWD
 // ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
 constexpr int FC1_KB = 9;   // k-steps per load batch (288 k-steps = 32 batches)
 constexpr int FC1_AROW = FC1_KB * 32 * 2 + 16;   // LDS bytes per staged pool row (padded)
@@ -358,6 +374,8 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
     }
 }
 
+#endif  // PDM_WANT_FC1_FWD
+#if PDM_WANT_FWD_REST
 // ---- head: fc1 reduce + bias + ReLU, fc2, CE, and (train) the head backward ----
 // One wave per batch row (HEAD_ROWS = 4 rows per workgroup, B/4 workgroups): lane j owns
 // hidden units 2j, 2j+1, so the fc2 logits are plain wave reductions and the split-K
@@ -514,8 +532,10 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
   PDM_STAMP(15);
 }
 
+#endif  // PDM_WANT_FWD_REST
 }  // namespace
 
+#if PDM_WANT_FWD_REST
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                     int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
@@ -528,12 +548,16 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
                                                      b2, pool, pmask, xg, ylab);
 }
 
+#endif
+#if PDM_WANT_FC1_FWD
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st) {
   dim3 grid(((B + 31) / 32) * splitk);
   fc1_fwd_kernel<<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);
 }
 
+#endif
+#if PDM_WANT_FWD_REST
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
@@ -559,3 +583,4 @@ void read_stamps_fwd(unsigned long long* host) {
   for (int i = 0; i < 256 * 16; ++i) host[i] = 0;
 }
 #endif
+#endif  // PDM_WANT_FWD_REST

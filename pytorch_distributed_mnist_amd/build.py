@@ -15,6 +15,7 @@ from __future__ import annotations
 import argparse
 import glob
 import hashlib
+import re
 import os
 import subprocess
 import sys
@@ -74,10 +75,32 @@ def compile_flags(abi: int, inc):
     return flags
 
 
+# Per-file compiler flags.  fc1_fwd / fc1_bwd are translation units of their own (wrappers
+# that include cnn_fwd.hip / cnn_bwd.hip with a section switch) so that they can use the
+# max-ilp machine scheduler, which measured faster for them and slower for cnn_fwd /
+# cnn_bwd (docs/kernels.md, tools/gpu_ab.sh).
+FILE_FLAGS = {
+    "kernels/fc1_fwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "kernels/fc1_bwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+}
+
+
+def _included_sources(path):
+    """.hip files a wrapper source #includes (their text is part of its object's hash)."""
+    out = []
+    with open(path) as f:
+        for line in f:
+            m = re.match(r'\s*#include\s+"([^"]+\.hip)"', line)
+            if m:
+                out.append(os.path.join(os.path.dirname(path), m.group(1)))
+    return out
+
+
 def _hash(path, flags, hdr_digest):
     h = hashlib.sha256()
-    with open(path, "rb") as f:
-        h.update(f.read())
+    for p in [path] + _included_sources(path):
+        with open(p, "rb") as f:
+            h.update(f.read())
     h.update(" ".join(flags).encode())
     h.update(hdr_digest)
     return h.hexdigest()[:20]
@@ -99,11 +122,13 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
         raise RuntimeError("no sources under csrc/")
 
     def one(src):
-        rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-        obj = os.path.join(OBJ_DIR, f"{rel}.{_hash(src, flags, hdr_digest)}.o")
+        relp = os.path.relpath(src, CSRC).replace(os.sep, "/")
+        fflags = flags + FILE_FLAGS.get(relp, [])
+        rel = relp.replace("/", "_")
+        obj = os.path.join(OBJ_DIR, f"{rel}.{_hash(src, fflags, hdr_digest)}.o")
         if os.path.exists(obj) and not force:
             return obj, None
-        cmd = [hipcc()] + flags + ["-c", src, "-o", obj + ".tmp"]
+        cmd = [hipcc()] + fflags + ["-c", src, "-o", obj + ".tmp"]
         if src.endswith(".hip"):
             cmd[1:1] = ["-x", "hip"]
         if verbose:
