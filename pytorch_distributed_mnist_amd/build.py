@@ -85,6 +85,16 @@ FILE_FLAGS = {
 }
 
 
+def file_flags():
+    """FILE_FLAGS, overridden per file by $PDM_FILE_FLAGS ("rel/path.hip=flags;..."; diagnostic
+    builds)."""
+    ff = dict(FILE_FLAGS)
+    for item in filter(None, os.environ.get("PDM_FILE_FLAGS", "").split(";")):
+        path, _, fl = item.partition("=")
+        ff[path.strip()] = fl.split()
+    return ff
+
+
 def _included_sources(path):
     """.hip files a wrapper source #includes (their text is part of its object's hash)."""
     out = []
@@ -123,7 +133,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
 
     def one(src):
         relp = os.path.relpath(src, CSRC).replace(os.sep, "/")
-        fflags = flags + FILE_FLAGS.get(relp, [])
+        fflags = flags + file_flags().get(relp, [])
         rel = relp.replace("/", "_")
         obj = os.path.join(OBJ_DIR, f"{rel}.{_hash(src, fflags, hdr_digest)}.o")
         if os.path.exists(obj) and not force:
@@ -163,7 +173,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     keep = set(objs)
     variant = custom_out or any(os.environ.get(k) for k in
                                      ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL",
-                                      "PDM_LIN_ROWS", "PDM_NT", "PDM_HIPCC_FLAGS"))
+                                      "PDM_LIN_ROWS", "PDM_NT", "PDM_HIPCC_FLAGS",
+                                      "PDM_FILE_FLAGS"))
     for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not variant else []:
         if o not in keep:
             try:
