@@ -18,18 +18,21 @@
 //             fc1 weight-gradient GEMM), fc1 bias partials; advances step counters.
 #include "cnn_common.h"
 
-// Translation-unit split: fc1_fwd is compiled from fc1_fwd.hip (this file with
-// PDM_FC1_FWD_TU = 1) under its own scheduler flags (build.py FILE_FLAGS); this file's own
-// compile holds cnn_fwd and the head.  PDM_STAMPS builds keep everything here.
-#ifndef PDM_FC1_FWD_TU
-#define PDM_FC1_FWD_TU 0
+// Translation-unit split: fc1_fwd and the head are compiled from fc1_fwd.hip / cnn_head.hip
+// (this file with PDM_FWD_TU = 1 / 2) under their own scheduler flags (build.py
+// FILE_FLAGS); this file's own compile holds cnn_fwd.  PDM_STAMPS builds keep everything
+// here (one stamp buffer).
+#ifndef PDM_FWD_TU
+#define PDM_FWD_TU 0
 #endif
 #if defined(PDM_STAMPS)
-#define PDM_WANT_FC1_FWD (PDM_FC1_FWD_TU == 0)
+#define PDM_WANT_FC1_FWD (PDM_FWD_TU == 0)
+#define PDM_WANT_HEAD (PDM_FWD_TU == 0)
 #else
-#define PDM_WANT_FC1_FWD (PDM_FC1_FWD_TU == 1)
+#define PDM_WANT_FC1_FWD (PDM_FWD_TU == 1)
+#define PDM_WANT_HEAD (PDM_FWD_TU == 2)
 #endif
-#define PDM_WANT_FWD_REST (PDM_FC1_FWD_TU == 0)
+#define PDM_WANT_FWD_REST (PDM_FWD_TU == 0)
 
 namespace {
 
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
 }
 
 #endif  // PDM_WANT_FC1_FWD
-#if PDM_WANT_FWD_REST
+#if PDM_WANT_HEAD
 // ---- head: fc1 reduce + bias + ReLU, fc2, CE, and (train) the head backward ----
 // One wave per batch row (HEAD_ROWS = 4 rows per workgroup, B/4 workgroups): lane j owns
 // hidden units 2j, 2j+1, so the fc2 logits are plain wave reductions and the split-K
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
   PDM_STAMP(15);
 }
 
-#endif  // PDM_WANT_FWD_REST
+#endif  // PDM_WANT_HEAD
 }  // namespace
 
 #if PDM_WANT_FWD_REST
@@ -557,7 +560,7 @@ void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, i
 }
 
 #endif
-#if PDM_WANT_FWD_REST
+#if PDM_WANT_HEAD
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
@@ -574,6 +577,8 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
 
 int cnn_head_blocks(int groups) { return groups < CNN_HEAD_MAX_BLOCKS ? groups : CNN_HEAD_MAX_BLOCKS; }
 
+#endif  // PDM_WANT_HEAD
+#if PDM_WANT_FWD_REST
 #ifdef PDM_STAMPS
 void read_stamps_fwd(unsigned long long* host) {
   hipMemcpyFromSymbol(host, HIP_SYMBOL(pdm_stamps), sizeof(unsigned long long) * 256 * 16);

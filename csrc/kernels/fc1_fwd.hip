@@ -1,4 +1,4 @@
 // fc1_fwd (kernel in cnn_fwd.hip) as its own translation unit, compiled with the max-ilp
-// machine scheduler (build.py FILE_FLAGS): in-step 5.6-5.8 -> 5.1-5.4 us at B = 256.
-#define PDM_FC1_FWD_TU 1
+// machine scheduler (build.py FILE_FLAGS): in-step 5.7 -> 5.3 us at B = 256.
+#define PDM_FWD_TU 1
 #include "cnn_fwd.hip"

@@ -82,6 +82,7 @@ def compile_flags(abi: int, inc):
 FILE_FLAGS = {
     "kernels/fc1_fwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "kernels/fc1_bwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "kernels/cnn_head.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
 
 
