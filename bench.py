@@ -1,22 +1,28 @@
 """Throughput benchmark: the flagship training step on N GPUs of one node.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model cnn|linear]
+                    [--scaling weak|strong|both]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Metric (BASELINE.json): images/sec for the whole node, MNIST CNN (SURVEY.md §7.1:
 conv 1->32 3x3 + ReLU, conv 32->64 3x3 + ReLU, maxpool 2, fc 9216->128 + ReLU,
-fc 128->10, log-softmax/NLL) trained with DDP (bucketed RCCL all-reduce over
-xGMI) and SGD-momentum, bf16 compute / fp32 master weights, on synthetic
-1x28x28 data of MNIST size (60k) with random-init weights.  Per-GPU batch is
-fixed (weak scaling): 256 images per rank by default, the reference's per-GPU
-batch at world_size 1 (its --batch-size 256 is split over the GPUs).
+fc 128->10, log-softmax/NLL) trained with DDP (bucketed all-reduce over xGMI) and
+SGD-momentum, bf16 compute / fp32 master weights, on synthetic 1x28x28 data of MNIST
+size (60k) with random-init weights.
 
-A timed step is the complete training step: batch gather + normalise,
-forward, loss, backward, gradient all-reduce, optimizer update (incl. the
-epoch-boundary reshuffles that fall inside the window).  W untimed warmup
-steps, then exactly K steps bracketed by a barrier + device synchronize on
-both sides; the slowest rank's time is reported.
+Two scaling modes (both measured by default, one JSON line):
+  weak   -- 256 images per rank (global batch 256 N): the headline `value`;
+  strong -- the reference's own DDP semantics: the node batch 256 is split over the
+            ranks (multi_proc_single_gpu.py:174, --batch-size 256 -> 128/64/32 per rank
+            at N = 2/4/8), reported under "strong" (at N = 1 the two coincide).
+
+A timed step is the complete training step: batch gather + normalise, forward, loss,
+backward, gradient all-reduce, optimizer update.  The timed window is placed so that an
+epoch boundary falls inside it (the next epoch's DistributedSampler order, prefetched on a
+host thread, is uploaded and gathered in stream order), i.e. the per-epoch data work is
+measured too.  W untimed warmup steps, then exactly K steps bracketed by a barrier +
+device synchronize on both sides; the slowest rank's time is reported.
 """
 from __future__ import annotations
 
@@ -28,12 +34,13 @@ import time
 
 import torch
 
-# The number to beat (BASELINE.md protocol): the reference's own training loop with the CNN
-# swapped in, PyTorch eager + DDP/RCCL on one MI355X (tools/reference_eager.py, DataLoader with
-# 4 workers, fp32, SGD momentum, batch 256; profiles/reference_eager_n1.jsonl).  For N GPUs
-# the baseline is taken as N x this value, i.e. perfect weak scaling of the reference.
+# The reference's own training loop with the CNN swapped in, PyTorch eager + DDP/RCCL on one
+# MI355X (tools/reference_eager.py, DataLoader with 4 workers, fp32, SGD momentum, batch 256;
+# profiles/reference_eager_n1.jsonl).  For N GPUs the baseline is taken as N x this value,
+# i.e. perfect weak scaling of the reference.
 REFERENCE_CNN_IMG_S_1GPU = 135369.5
 REFERENCE_LINEAR_IMG_S_1GPU = 221060.4
+NODE_BATCH = 256          # reference --batch-size default (node total, S:297-300)
 
 
 def parse():
@@ -42,11 +49,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--model", choices=["cnn", "linear"], default="cnn")
-    ap.add_argument("--batch-per-rank", type=int, default=256)
+    ap.add_argument("--batch-per-rank", type=int, default=NODE_BATCH,
+                    help="per-rank batch of the weak-scaling measurement")
+    ap.add_argument("--scaling", choices=["weak", "strong", "both"], default="both")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default=None)
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--no-graphs", dest="graphs", action="store_false")
     ap.add_argument("--train-size", type=int, default=60000)
+    ap.add_argument("--timeout", type=float, default=600.0,
+                    help="deadline (s) for RCCL init and every host sync")
     return ap.parse_args()
 
 
@@ -55,38 +66,39 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws != a.gpus:
-        if ws == 1 and a.gpus > 1:
-            print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} procs",
-                  file=sys.stderr)
-            sys.exit(2)
+    if ws != a.gpus and ws == 1 and a.gpus > 1:
+        print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} procs",
+              file=sys.stderr)
+        sys.exit(2)
+    from types import SimpleNamespace
+
     from pytorch_distributed_mnist_amd import parallel
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
-    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.data.sampler import EpochIndexPrefetcher
     from pytorch_distributed_mnist_amd.models.reference import MODULES
     from pytorch_distributed_mnist_amd.models.specs import get_spec
     from pytorch_distributed_mnist_amd.optim.flat import build_optimizer
     from pytorch_distributed_mnist_amd.runtime.arena import FlatArena
     from pytorch_distributed_mnist_amd.runtime.program import TrainProgram
-    from types import SimpleNamespace
 
     device = parallel.pick_device(local_rank, "cuda")
     # PDM_BENCH_BACKEND=gloo: rehearsal of the multi-rank flow on a single GPU (with
     # PDM_SHARE_DEVICE=1); the measured configuration is always nccl = RCCL
     backend = os.environ.get("PDM_BENCH_BACKEND", "nccl")
     ctx = parallel.init_distributed(backend, "env://" if ws > 1 else None, ws, rank, local_rank,
-                                    device, init_pg=ws > 1)
-    # PDM_FORCE_COMM=1 at N=1: run the multi-GPU step structure (unfused conv reduction,
-    # grouped RCCL all-reduce through a 1-rank communicator) to price it without transfers
+                                    device, timeout_s=a.timeout, init_pg=ws > 1)
+    # PDM_FORCE_COMM=1 at N=1: run the multi-GPU step structure (conv reduction, bucket
+    # all-reduces through a 1-rank communicator) to price it without transfers
     force_comm = os.environ.get("PDM_FORCE_COMM") == "1"
-    comm = parallel.make_comm(ctx, force_native=force_comm)
     model = a.model
+    spec = get_spec(model)
+    parallel.verify_params_across_ranks(spec, rank, ws)
+    comm = parallel.make_comm(ctx, force_native=force_comm)
     dtype = "bf16" if model == "cnn" else "fp32"
     optname = a.optimizer or ("sgd" if model == "cnn" else "adam")
     lr = a.lr if a.lr is not None else (0.01 if optname == "sgd" else 1e-3)
 
     torch.manual_seed(1234 + rank)
-    spec = get_spec(model)
     arena = FlatArena(spec, device)
     arena.load_module(MODULES[model]())
     comm.broadcast_(arena.params, 0)
@@ -94,132 +106,191 @@ def main():
     bounds = spec.bucket_bounds()
     # Gradient transports to choose from: with $PDM_COMM unset (auto) on the RCCL data plane
     # both the direct xGMI all-reduce and RCCL are built, and a short untimed calibration
-    # run of the real step picks the faster one for this N (agreed over ranks).
+    # run of the real step picks the faster one for this N and batch (agreed over ranks).
     want = os.environ.get("PDM_COMM", "auto")
     reducers = {}
+    notes = []
     if (ws > 1 or force_comm) and want == "auto" and isinstance(comm, parallel.RcclComm):
         try:
             reducers["xgmi"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
                                                     transport="xgmi")
         except Exception as e:                # collective decision: no rank uses xgmi
+            notes.append(f"xgmi unavailable: {e}")
             print(f"bench.py: xgmi transport unavailable: {e}", file=sys.stderr, flush=True)
         reducers["rccl"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
                                                 transport="rccl")
     else:
         r0 = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm, transport=want)
         reducers[r0.kind] = r0
+        if r0.transport_note:
+            notes.append(r0.transport_note)
     train = synthetic_split(a.train_size, True)
     test = synthetic_split(1024, False)
-    B = a.batch_per_rank
-    first = next(iter(reducers.values()))
-    prog = TrainProgram(model, dtype, arena, opt, first, train, test, B, use_graphs=a.graphs)
     n = len(train)
+    prefetch = EpochIndexPrefetcher(n, ws, rank)
+    first = next(iter(reducers.values()))
 
-    state = {"epoch": 0, "step": 0}
-
-    def next_epoch():
-        prog.set_train_indices(distributed_indices(n, ws, rank, state["epoch"]))
-        prog.gpu.begin_epoch()
-        state["epoch"] += 1
-        state["step"] = 0
-
-    per_rank = -(-n // ws)
-    full = per_rank // B                       # full-batch steps per epoch
-
-    def run(k):
-        while k > 0:
-            if state["step"] >= full:
-                next_epoch()
-            m = min(k, full - state["step"])
-            prog.gpu.train_steps(B, m)
-            state["step"] += m
-            k -= m
+    def sync(what):
+        parallel.bounded_sync(device, a.timeout, comm, what)
 
     def barrier():
         parallel.control_barrier()      # gloo (CPU tensor): no torch NCCL communicator
 
-    def timed(k):
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        run(k)
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
+    def allmax(x: float) -> float:
         if ws > 1:
-            t = torch.tensor([el], dtype=torch.float64)
+            t = torch.tensor([x], dtype=torch.float64)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            el = float(t.item())
-        return el
+            x = float(t.item())
+        return x
 
-    def use(red):
-        prog.reducer = red
-        prog.gpu.reducer = red
-        prog.gpu.use_graphs = bool(a.graphs) and red.capturable
-        prog.gpu.invalidate_graphs()
+    def measure(B: int) -> dict:
+        """Calibrate the transport for per-rank batch B, then time a.steps steps."""
+        prog = TrainProgram(model, dtype, arena, opt, first, train, test, B, use_graphs=a.graphs)
+        full = -(-n // ws) // B                    # full-batch steps per epoch
+        state = {"epoch": 0, "step": 0}
 
-    opt.sync_hyperparams()
-    next_epoch()
-    calib = {}
-    if len(reducers) > 1:
-        for name, red in reducers.items():
-            use(red)
-            run(16)
-            calib[name] = timed(48) / 48 * 1e3
-            try:
-                red.check()
-                ok = 1
-            except RuntimeError as e:
-                print(f"bench.py: {name} transport failed calibration: {e}", file=sys.stderr,
-                      flush=True)
-                ok = 0
-            if ws > 1:                         # every rank drops a transport any rank saw fail
-                t = torch.tensor([ok], dtype=torch.int32)
-                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
-                ok = int(t.item())
-            if not ok:
-                if name == "rccl":
-                    raise RuntimeError("rccl transport failed calibration")
-                del calib[name]
-                torch.cuda.synchronize()
-                # replicas (and their momentum) may differ after a failed reduce
-                for t in (arena.params, *opt.state_buffers().values()):
-                    comm.broadcast_(t, 0)
-                if hasattr(prog.gpu, "refresh_shadows"):
-                    prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
-        best = min(calib, key=calib.get)
-        use(reducers[best])
-    chosen = prog.reducer
-    # capture + upload the step graphs outside the timed window (a graph captured lazily
-    # on first use would put its capture inside a short timed run)
-    prog.gpu.prepare(B)
-    run(a.warmup)
-    elapsed = timed(a.steps)
-    chosen.check()
-    if not torch.isfinite(arena.params).all():
-        raise RuntimeError("non-finite parameters after the benchmark")
-    ms = elapsed / a.steps * 1e3
-    global_batch = B * ws
-    value = a.steps * global_batch / elapsed
+        def next_epoch():
+            prog.set_train_indices(prefetch.get(state["epoch"]))
+            prog.gpu.begin_epoch()
+            state["epoch"] += 1
+            state["step"] = 0
+
+        def run(k):
+            while k > 0:
+                if state["step"] >= full:
+                    next_epoch()
+                m = min(k, full - state["step"])
+                prog.gpu.train_steps(B, m)
+                state["step"] += m
+                k -= m
+
+        def timed(k):
+            sync("warmup")
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(k)
+            sync("timed steps")
+            barrier()
+            torch.cuda.synchronize()
+            return allmax(time.perf_counter() - t0)
+
+        def use(red):
+            prog.reducer = red
+            prog.gpu.reducer = red
+            prog.gpu.use_graphs = bool(a.graphs) and red.capturable
+            prog.gpu.invalidate_graphs()
+
+        opt.sync_hyperparams()
+        next_epoch()
+        calib = {}
+        if len(reducers) > 1:
+            for name, red in reducers.items():
+                use(red)
+                run(16)
+                calib[name] = timed(48) / 48 * 1e3
+                try:
+                    red.check()
+                    ok = 1
+                except RuntimeError as e:
+                    print(f"bench.py: {name} transport failed calibration: {e}", file=sys.stderr,
+                          flush=True)
+                    notes.append(f"{name} failed calibration at B={B}: {e}")
+                    ok = 0
+                if ws > 1:                     # every rank drops a transport any rank saw fail
+                    t = torch.tensor([ok], dtype=torch.int32)
+                    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+                    ok = int(t.item())
+                if not ok:
+                    if name == "rccl":
+                        raise RuntimeError("rccl transport failed calibration")
+                    del calib[name]
+                    sync("recovery")
+                    # replicas (and their momentum) may differ after a failed reduce
+                    for t in (arena.params, *opt.state_buffers().values()):
+                        comm.broadcast_(t, 0)
+                    if hasattr(prog.gpu, "refresh_shadows"):
+                        prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
+            best = min(calib, key=calib.get)
+            use(reducers[best])
+        else:
+            use(first)
+        chosen = prog.reducer
+        # capture + upload the step graphs outside the timed window (a graph captured lazily
+        # on first use would put its capture inside a short timed run)
+        prog.gpu.prepare(B)
+        run(a.warmup)
+        # put the next epoch boundary inside the timed window: continue the current epoch
+        # from the step that leaves K // 2 full steps before the boundary (every step is the
+        # same kernel chain on a different batch of the sampler order)
+        left = full - state["step"]
+        if a.steps >= 2 and left > a.steps // 2:
+            skip = left - a.steps // 2
+            sync("reposition")
+            prog.gpu.ctr[0] += skip            # device data-step counter
+            state["step"] += skip
+        left = full - state["step"]
+        boundaries = -(-(a.steps - left) // full) if a.steps > left else 0
+        elapsed = timed(a.steps)
+        chosen.check()
+        if not torch.isfinite(arena.params).all():
+            raise RuntimeError("non-finite parameters after the benchmark")
+        ms = elapsed / a.steps * 1e3
+        return {"B": B, "global_batch": B * ws, "elapsed": elapsed, "ms": ms,
+                "value": a.steps * B * ws / elapsed, "transport": chosen.kind,
+                "calib": {k: round(v, 5) for k, v in calib.items()},
+                "graphs": bool(prog.gpu.use_graphs), "epoch_boundaries_timed": boundaries}
+
+    strong_B = max(1, NODE_BATCH // ws)
+    res = {}
+    if a.scaling in ("weak", "both"):
+        res["weak"] = measure(a.batch_per_rank)
+    if a.scaling in ("strong", "both"):
+        if "weak" in res and strong_B == a.batch_per_rank:
+            res["strong"] = res["weak"]
+        else:
+            res["strong"] = measure(strong_B)
+    main_mode = "weak" if "weak" in res else "strong"
+    m = res[main_mode]
+
+    comm_info = {"data_plane": type(comm).__name__, "world_size": ws}
+    if isinstance(comm, parallel.RcclComm):
+        comm_info["rccl_comm_count"] = comm.comm_count()      # ranks RCCL itself reports
+        comm_info["rccl_version"] = int(__import__(
+            "pytorch_distributed_mnist_amd.ops._ext", fromlist=["x"]).require().rccl_version())
+    if "xgmi" in reducers:
+        comm_info["xgmi_peers_mapped"] = int(reducers["xgmi"]._native.peers_mapped()) \
+            if reducers["xgmi"]._native is not None else 0
+    if notes:
+        comm_info["fallback"] = notes
     if rank == 0:
-        print(json.dumps({
+        ref = REFERENCE_CNN_IMG_S_1GPU if model == "cnn" else REFERENCE_LINEAR_IMG_S_1GPU
+        line = {
             "metric": "images/sec (whole node) MNIST CNN DDP at 1/2/4/8 MI355X"
             if model == "cnn" else "images/sec (whole node) MNIST Linear DDP",
-            "value": round(value, 1), "unit": "images/sec", "n_gpus": ws, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": round(value / (ws * (
-                REFERENCE_CNN_IMG_S_1GPU if model == "cnn" else REFERENCE_LINEAR_IMG_S_1GPU)), 3),
+            "value": round(m["value"], 1), "unit": "images/sec", "n_gpus": ws, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(m["ms"], 5), "higher_is_better": True,
+            "scaling": main_mode, "vs_baseline": round(m["value"] / (ws * ref), 3),
             "dtype": dtype,
             "data": "synthetic (60k x 1x28x28 uint8, MNIST-shaped), random-init weights",
             "config": {"model": "mnist_cnn" if model == "cnn" else "mnist_linear",
-                       "global_batch": global_batch, "batch_per_rank": B, "seq_len": None,
-                       "parallelism": f"dp{ws}", "optimizer": optname,
-                       "graphs": bool(prog.gpu.use_graphs), "grad_transport": chosen.kind,
-                       "transport_calibration_ms_per_step":
-                           {k: round(v, 5) for k, v in calib.items()}},
-        }), flush=True)
+                       "global_batch": m["global_batch"], "batch_per_rank": m["B"],
+                       "seq_len": None, "parallelism": f"dp{ws}", "optimizer": optname,
+                       "graphs": m["graphs"], "grad_transport": m["transport"],
+                       "transport_calibration_ms_per_step": m["calib"],
+                       "epoch_boundaries_timed": m["epoch_boundaries_timed"]},
+            "comm": comm_info,
+        }
+        if main_mode == "weak" and "strong" in res:
+            s = res["strong"]
+            line["strong"] = {"value": round(s["value"], 1), "ms_per_step": round(s["ms"], 5),
+                              "global_batch": s["global_batch"], "batch_per_rank": s["B"],
+                              "grad_transport": s["transport"],
+                              "transport_calibration_ms_per_step": s["calib"],
+                              "epoch_boundaries_timed": s["epoch_boundaries_timed"],
+                              "semantics": "reference DDP: node batch 256 split over ranks (S:174)"}
+        print(json.dumps(line), flush=True)
+    prefetch.close()
     for red in reducers.values():
         red.close()
     comm.close()

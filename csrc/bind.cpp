@@ -436,7 +436,7 @@ static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   TORCH_CHECK(u.numel == (int64_t)CNN_HID * CNN_FEAT && g.numel() == u.numel &&
                   m.numel() == u.numel && sh.numel() == u.numel, "fc_update: fc1 weight sizes");
   for (const void* q : {p.data_ptr(), g.data_ptr(), m.data_ptr()}) need_aligned(q, 16, "fc_update fp32");
-  need_aligned(sh.data_ptr(), 8, "fc_update shadow");
+  need_aligned(sh.data_ptr(), 16, "fc_update shadow");   // fc1_bwd stores it as 16-B uint4
   u.p = p.data_ptr<float>();
   u.g = g.data_ptr<float>();
   u.m = m.data_ptr<float>();

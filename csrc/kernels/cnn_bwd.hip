@@ -974,11 +974,15 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
                     const FcUpdate& fcu, hipStream_t st) {
   const int nd = (ldt / 32) * DX_TILES;
   int nblk = DW_TILES + nd + HR_BLOCKS, off = 0;
-  // diagnostic only (tools/kbench.py): PDM_FC1BWD_ROLE=dw|dx|hr launches one role alone
+#ifdef PDM_DIAG_ROLES
+  // diagnostic builds only (tools/kbench_fc.py): PDM_FC1BWD_ROLE=dw|dx|hr launches one
+  // role alone.  Never compiled into the production extension: a stray environment
+  // variable there would silently skip gradient work (and the fused fc1 update).
   static const char* role = getenv("PDM_FC1BWD_ROLE");
   if (role && role[0] == 'd' && role[1] == 'w') nblk = DW_TILES;
   else if (role && role[0] == 'd' && role[1] == 'x') { nblk = nd; off = DW_TILES; }
   else if (role && role[0] == 'h') { nblk = HR_BLOCKS; off = DW_TILES + nd; }
+#endif
   fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, dht, ldt, pool, wf1t, B, gwf1, dpool, head_slab,
                                        head_blocks, gwf2, gbf2, gbf1, metrics, off, fcu);
 }

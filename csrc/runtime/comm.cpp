@@ -15,11 +15,23 @@
 //
 // RCCL resolution: the extension links torch's bundled librccl.so (SONAME
 // librccl.so.1), so the process has exactly one RCCL — the one torch loaded.
+//
+// Failure detection: the communicator is created NON-BLOCKING
+// (ncclCommInitRankConfig, config.blocking = 0) and the host polls
+// ncclCommGetAsyncError against a deadline (the app's --timeout), so a rank that
+// never joins makes every other rank raise instead of hanging the node; the
+// communicator is aborted (ncclCommAbort) on the way out.  Enqueue calls that
+// report ncclInProgress are polled against the same deadline.  Device-side hangs of
+// an enqueued collective are bounded at the host's sync points by
+// parallel.comm.bounded_sync, which aborts the communicator (unblocking its
+// kernels) once the deadline passes.
 #include <c10/hip/HIPStream.h>
 #include <rccl/rccl.h>
 #include <torch/extension.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -63,13 +75,32 @@ py::bytes rccl_unique_id() {
 
 class RcclComm {
  public:
-  RcclComm(const std::string& uid, int rank, int nranks, int device)
-      : rank_(rank), nranks_(nranks), device_(device) {
+  RcclComm(const std::string& uid, int rank, int nranks, int device, double timeout_s)
+      : rank_(rank), nranks_(nranks), device_(device), timeout_s_(timeout_s) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad unique id size ", uid.size());
+    TORCH_CHECK(timeout_s > 0, "RCCL timeout must be positive");
     ncclUniqueId id;
     memcpy(&id, uid.data(), sizeof(id));
     HIP_OK(hipSetDevice(device));
-    NCCL_OK(ncclCommInitRank(&comm_, nranks, id, rank));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;   // init returns at once; completion is polled against the deadline
+    ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      TORCH_CHECK(false, "RCCL error ", ncclGetErrorString(r), " at ncclCommInitRankConfig (rank ",
+                  rank, " of ", nranks, ")");
+    }
+    ncclResult_t st = settle("communicator init");
+    if (st != ncclSuccess) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+      TORCH_CHECK(false, "RCCL communicator init failed on rank ", rank, " of ", nranks, ": ",
+                  st == ncclInProgress ? "timed out after " + std::to_string(timeout_s) +
+                                             " s waiting for the other ranks (a peer never joined "
+                                             "or died during bring-up)"
+                                       : std::string(ncclGetErrorString(st)));
+    }
     int lo = 0, hi = 0;
     HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     // highest priority: collectives should not queue behind compute kernels
@@ -84,11 +115,68 @@ class RcclComm {
       hipStreamSynchronize(stream_);
       ncclCommDestroy(comm_);
       comm_ = nullptr;
-      hipEventDestroy(ev_in_);
-      hipEventDestroy(ev_out_);
-      hipStreamDestroy(stream_);
+      release_stream();
     }
   }
+
+  // Tear the communicator down without waiting for in-flight work: RCCL's abort flag
+  // makes kernels that wait for a missing peer exit (used after a timeout).
+  void abort() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+      release_stream();
+    }
+  }
+
+  // Poll the communicator's async state until it leaves ncclInProgress or the deadline
+  // passes; returns the final state (ncclInProgress = timed out).
+  ncclResult_t settle(const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t st = ncclInProgress;
+    for (int i = 0;; ++i) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return ncclInternalError;
+      if (st != ncclInProgress) return st;
+      const double el =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s_) return ncclInProgress;
+      std::this_thread::sleep_for(std::chrono::microseconds(i < 100 ? 10 : 1000));
+    }
+    (void)what;
+  }
+
+  // result of an enqueue call on the non-blocking communicator
+  void enqueued(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) r = settle(what);
+    if (r == ncclInProgress) {
+      abort();
+      TORCH_CHECK(false, "RCCL ", what, " timed out after ", timeout_s_, " s (rank ", rank_, " of ",
+                  nranks_, "); communicator aborted");
+    }
+    TORCH_CHECK(r == ncclSuccess, "RCCL error ", ncclGetErrorString(r), " at ", what);
+  }
+
+  // ranks / device as the communicator itself reports them
+  int comm_count() {
+    alive();
+    int n = 0;
+    NCCL_OK(ncclCommCount(comm_, &n));
+    return n;
+  }
+  int comm_user_rank() {
+    alive();
+    int r = -1;
+    NCCL_OK(ncclCommUserRank(comm_, &r));
+    return r;
+  }
+  // ncclSuccess (0) while healthy; an RCCL error code once something failed asynchronously
+  int async_error() {
+    if (!comm_) return (int)ncclInvalidUsage;
+    ncclResult_t st = ncclSuccess;
+    NCCL_OK(ncclCommGetAsyncError(comm_, &st));
+    return (int)st;
+  }
+  double timeout_s() const { return timeout_s_; }
 
   hipStream_t caller() const { return c10::hip::getCurrentHIPStream(device_).stream(); }
 
@@ -108,13 +196,14 @@ class RcclComm {
     alive();
     hipStream_t cur = caller();
     fork(cur);
-    NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), ncclSum, comm_,
-                          stream_));
+    enqueued(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), ncclSum, comm_,
+                           stream_), "all-reduce");
     join(cur);
   }
 
   void all_reduce_range(void* ptr, size_t count, ncclDataType_t dt) {
-    NCCL_OK(ncclAllReduce(ptr, ptr, count, dt, ncclSum, comm_, stream_));
+    alive();
+    enqueued(ncclAllReduce(ptr, ptr, count, dt, ncclSum, comm_, stream_), "bucket all-reduce");
   }
 
   void broadcast_(at::Tensor t, int root) {
@@ -122,8 +211,8 @@ class RcclComm {
     alive();
     hipStream_t cur = caller();
     fork(cur);
-    NCCL_OK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_,
-                          stream_));
+    enqueued(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_,
+                           stream_), "broadcast");
     join(cur);
   }
 
@@ -135,7 +224,8 @@ class RcclComm {
     at::Tensor out = at::empty(sizes, t.options());
     hipStream_t cur = caller();
     fork(cur);
-    NCCL_OK(ncclAllGather(t.data_ptr(), out.data_ptr(), t.numel(), nccl_dtype(t), comm_, stream_));
+    enqueued(ncclAllGather(t.data_ptr(), out.data_ptr(), t.numel(), nccl_dtype(t), comm_, stream_),
+             "all-gather");
     join(cur);
     return out;
   }
@@ -148,8 +238,16 @@ class RcclComm {
   hipStream_t stream() const { return stream_; }
 
  private:
-  void alive() const { TORCH_CHECK(comm_ != nullptr, "communicator destroyed"); }
+  void alive() const { TORCH_CHECK(comm_ != nullptr, "communicator destroyed or aborted"); }
+  void release_stream() {
+    if (ev_in_) hipEventDestroy(ev_in_);
+    if (ev_out_) hipEventDestroy(ev_out_);
+    if (stream_) hipStreamDestroy(stream_);
+    ev_in_ = ev_out_ = nullptr;
+    stream_ = nullptr;
+  }
   int rank_, nranks_, device_;
+  double timeout_s_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
@@ -200,7 +298,7 @@ class GradReducer {
     NCCL_OK(ncclGroupStart());
     for (size_t i = 0; i < starts_.size(); ++i)
       comm_.all_reduce_range(grads_.data_ptr<float>() + starts_[i], (size_t)counts_[i], ncclFloat32);
-    NCCL_OK(ncclGroupEnd());
+    comm_.enqueued(ncclGroupEnd(), "grouped bucket all-reduce");
     for (auto& e : reduced_) HIP_OK(hipEventRecord(e, comm_.stream()));
     pending_ = true;
   }
@@ -239,9 +337,15 @@ void register_comm(py::module& m) {
     return v;
   });
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init<const std::string&, int, int, int>(), py::arg("uid"), py::arg("rank"),
-           py::arg("nranks"), py::arg("device"))
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("uid"), py::arg("rank"),
+           py::arg("nranks"), py::arg("device"), py::arg("timeout_s") = 1800.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("all_reduce_", &RcclComm::all_reduce_)
+      .def("abort", &RcclComm::abort)
+      .def("comm_count", &RcclComm::comm_count)
+      .def("comm_user_rank", &RcclComm::comm_user_rank)
+      .def("async_error", &RcclComm::async_error)
+      .def_property_readonly("timeout_s", &RcclComm::timeout_s)
       .def("broadcast_", &RcclComm::broadcast_)
       .def("all_gather", &RcclComm::all_gather)
       .def("synchronize", &RcclComm::synchronize)

@@ -258,6 +258,13 @@ class XgmiReducer {
   int64_t first_error() { return read_err_words().second; }
 
 
+  // peers whose buffers this rank has mapped through hipIpc (own rank excluded)
+  int peers_mapped() const {
+    int n = 0;
+    for (int r = 0; r < nranks_; ++r) n += (r != rank_ && peers_[r] != nullptr);
+    return n;
+  }
+
   py::list describe() const {
     py::list out;
     for (const auto& c : ch_) {
@@ -374,6 +381,7 @@ void register_xgmi(py::module& m) {
       .def("error", &XgmiReducer::error)
       .def("first_error", &XgmiReducer::first_error)
       .def("describe", &XgmiReducer::describe)
+      .def("peers_mapped", &XgmiReducer::peers_mapped)
       .def("close", &XgmiReducer::close)
       .def_property_readonly("num_buckets", &XgmiReducer::num_buckets);
 }

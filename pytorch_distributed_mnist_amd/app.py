@@ -116,6 +116,9 @@ def run(args):
     spec = get_spec(args.arch)
     arena = FlatArena(spec, device)
     arena.load_module(MODULES[args.arch]())
+    # DDP construction: every rank must hold the same model before rank 0's weights are
+    # broadcast (reference :188-189, DDP's _verify_param_shape_across_processes)
+    parallel.verify_params_across_ranks(spec, rank, world_size)
     comm = parallel.make_comm(ctx)
     comm.broadcast_(arena.params, 0)
 
@@ -142,6 +145,10 @@ def run(args):
     dtype = resolve_dtype(args.dtype, args.arch, device)
     program = TrainProgram(args.arch, dtype, arena, optimizer, reducer, train_split, test_split,
                            args.batch_size, use_graphs=args.graphs)
+    if device.type == "cuda":
+        # every host sync of the epoch loop waits at most --timeout for the device (and the
+        # collectives it is queued behind), then aborts the communicator and raises
+        program.sync_fn = lambda what: parallel.bounded_sync(device, args.timeout, comm, what)
     trainer = Trainer(program)
 
     try:
@@ -150,14 +157,13 @@ def run(args):
             out('test loss: {}, test acc: {}.'.format(test_loss, test_acc))
             return
 
+        # epoch e+1's sample order is computed on a host thread while epoch e trains
+        prefetch = sampler.EpochIndexPrefetcher(len(train_split), world_size, rank)
         for epoch in range(args.start_epoch, args.epochs):
             with trace.range("epoch {}".format(epoch)):
-                with trace.range("sampler upload"):
-                    program.set_train_indices(
-                        sampler.distributed_indices(len(train_split), world_size, rank, epoch))
                 adjust_learning_rate(optimizer, epoch, args)
 
-                train_loss, train_acc = trainer.train()
+                train_loss, train_acc = trainer.train(prefetch.get(epoch))
                 reducer.check()             # xgmi: raise if a peer never arrived
                 test_loss, test_acc = trainer.evaluate()
 
@@ -177,8 +183,16 @@ def run(args):
                         save_checkpoint(make_state(epoch + 1, arena, best_acc, optimizer), is_best,
                                         epoch, directory=args.checkpoint_dir)
     finally:
+        if 'prefetch' in locals():
+            prefetch.close()
         if device.type == "cuda":
-            torch.cuda.synchronize(device)
+            import sys
+            pending = sys.exc_info()[1] is not None
+            try:
+                parallel.bounded_sync(device, args.timeout, comm, "teardown")
+            except RuntimeError:
+                if not pending:       # do not mask the error that is already propagating
+                    raise
         reducer.close()
         comm.close()
         parallel.shutdown()

@@ -67,6 +67,8 @@ def compile_flags(abi: int, inc):
         flags.append("-DPDM_DEBUG_BOUNDS=1")
     if os.environ.get("PDM_STAMPS"):
         flags.append("-DPDM_STAMPS=1")
+    if os.environ.get("PDM_DIAG_ROLES"):                   # fc1_bwd single-role launches
+        flags.append("-DPDM_DIAG_ROLES=1")
     for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS", "PDM_NT"):   # tuning experiments (diagnostic builds)
         if os.environ.get(k):
             flags.append(f"-D{k}={int(os.environ[k])}")
@@ -173,7 +175,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     # drop stale objects of sources that no longer exist / older hashes
     keep = set(objs)
     variant = custom_out or any(os.environ.get(k) for k in
-                                     ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL",
+                                     ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DIAG_ROLES", "PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL",
                                       "PDM_LIN_ROWS", "PDM_NT", "PDM_HIPCC_FLAGS",
                                       "PDM_FILE_FLAGS"))
     for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not variant else []:

@@ -78,7 +78,8 @@ def build_parser() -> argparse.ArgumentParser:
                         '(default, or $PDM_COMM) = xgmi when every rank passes its self-check')
     g.add_argument('--checkpoint-dir', default='checkpoints')
     g.add_argument('--timeout', type=float, default=1800.0,
-                   help='process-group / rendezvous timeout in seconds')
+                   help='deadline in seconds for the rendezvous, RCCL communicator init and every '
+                        'host sync on the device (a missing peer raises instead of hanging)')
     g.add_argument('--perf', action='store_true',
                    help='print an extra per-epoch throughput line on rank 0')
     g.add_argument('--trace', action='store_true',

@@ -25,10 +25,16 @@ class Trainer:
         if self.program.is_gpu:
             torch.cuda.synchronize(self.program.device)
 
-    def train(self):
+    def train(self, indices=None):
+        """One training epoch.  ``indices``: this rank's sample order for the epoch (the
+        reference's ``set_epoch`` reshuffle, :231), installed inside the timed region so the
+        epoch time includes the boundary work (index upload + epoch gather)."""
         self._sync()
         t0 = time.perf_counter()
         with trace.range("train"):
+            if indices is not None:
+                with trace.range("sampler upload"):
+                    self.program.set_train_indices(indices)
             result = self.program.train_epoch()   # reading the metrics synchronises
         self.last_train_seconds = time.perf_counter() - t0
         return result

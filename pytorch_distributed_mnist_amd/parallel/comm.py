@@ -15,6 +15,7 @@ process group (bench at N=1): every collective is the identity.
 from __future__ import annotations
 
 import itertools
+import time
 
 import torch
 import torch.distributed as dist
@@ -67,10 +68,14 @@ class TorchComm(Communicator):
 
 
 class RcclComm(Communicator):
-    """Native RCCL communicator over xGMI on a dedicated HIP stream."""
+    """Native RCCL communicator over xGMI on a dedicated HIP stream.
+
+    Created non-blocking with a deadline (``timeout_s``, the app's ``--timeout``): a rank
+    that never joins makes the others raise instead of hanging (csrc/runtime/comm.cpp)."""
     native = True
 
-    def __init__(self, rank: int, world_size: int, device: torch.device, tag: str | None = None):
+    def __init__(self, rank: int, world_size: int, device: torch.device, tag: str | None = None,
+                 timeout_s: float = 1800.0):
         C = _ext.require()
         self.rank, self.world_size = rank, world_size
         if tag is None:
@@ -85,11 +90,22 @@ class RcclComm(Communicator):
                 uid = store.get(key)
         else:
             uid = C.rccl_unique_id()
-        self._c = C.RcclComm(bytes(uid), rank, world_size, device.index or 0)
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        self._c = C.RcclComm(bytes(uid), rank, world_size, dev, float(timeout_s))
+        self.timeout_s = float(timeout_s)
 
     @property
     def handle(self):
         return self._c
+
+    def comm_count(self) -> int:
+        """Number of ranks as the RCCL communicator itself reports them (ncclCommCount)."""
+        return int(self._c.comm_count())
+
+    def abort(self) -> None:
+        if self._c is not None:
+            self._c.abort()
+            self._c = None
 
     def all_reduce_(self, t):
         self._c.all_reduce_(t)
@@ -105,12 +121,39 @@ class RcclComm(Communicator):
             self._c = None
 
 
+def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | None = None,
+                 what: str = "device work") -> None:
+    """``torch.cuda.synchronize`` with a deadline.
+
+    Everything queued on the current stream (kernels, hipGraph replays, the RCCL
+    collectives they wait on) must finish within ``timeout_s``; otherwise the RCCL
+    communicator is aborted (its kernels waiting for a dead peer exit) and this raises.
+    This is what bounds a collective that hangs on the device: the reference inherits
+    the same semantics from torch's NCCL watchdog (process-group timeout)."""
+    if device.type != "cuda":
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    t0 = time.monotonic()
+    delay = 1e-5
+    while not ev.query():
+        if time.monotonic() - t0 > timeout_s:
+            if isinstance(comm, RcclComm):
+                comm.abort()
+            raise RuntimeError(f"{what} did not finish within {timeout_s:.0f} s (a peer rank is "
+                               f"missing or hung); communicator aborted")
+        time.sleep(delay)
+        delay = min(delay * 2, 1e-3)
+    torch.cuda.synchronize(device)
+
+
 def make_comm(ctx, force_native: bool = False) -> Communicator:
     """Pick the data-plane communicator for a rank's DistContext."""
     if ctx.world_size == 1 and not force_native and not ctx.initialized:
         return LocalComm()
     if ctx.is_gpu and ctx.backend == "nccl":
-        return RcclComm(ctx.rank, ctx.world_size, ctx.device)
+        return RcclComm(ctx.rank, ctx.world_size, ctx.device,
+                        timeout_s=getattr(ctx, "timeout_s", 1800.0))
     if ctx.initialized:
         return TorchComm()
     return LocalComm()

@@ -39,6 +39,7 @@ class DistContext:
     backend: str            # user-facing: "nccl" or "gloo"
     device: torch.device
     initialized: bool
+    timeout_s: float = 1800.0     # --timeout: rendezvous, RCCL init and bounded host syncs
 
     @property
     def is_gpu(self) -> bool:
@@ -85,7 +86,7 @@ def init_distributed(backend: str, init_method: Optional[str], world_size: int, 
     elif distributed_is_initialized():
         initialized = True
     return DistContext(rank=rank, world_size=world_size, local_rank=local_rank, backend=backend,
-                       device=device, initialized=initialized)
+                       device=device, initialized=initialized, timeout_s=float(timeout_s))
 
 
 def control_barrier() -> None:

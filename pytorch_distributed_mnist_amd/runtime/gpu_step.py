@@ -121,7 +121,9 @@ class GpuStepBase:
                 exe = g.raw_cuda_graph_exec()
             except (AttributeError, RuntimeError):
                 continue
-            self.C.graph_upload(int(exe), self.device.index or 0)
+            dev = self.device.index if self.device.index is not None else \
+                torch.cuda.current_device()
+            self.C.graph_upload(int(exe), dev)
         torch.cuda.synchronize(self.device)
 
     def train_steps(self, B: int, n: int) -> None:

@@ -44,6 +44,9 @@ class TrainProgram:
         self.test_split = test_split
         self.train_idx_cpu: Optional[torch.Tensor] = None
         self._bounds = []
+        # host sync before the once-per-epoch metric read: set by the app to a bounded
+        # wait (parallel.bounded_sync) so a hung collective raises after --timeout
+        self.sync_fn = None
         if self.is_gpu:
             from .gpu_step import make_gpu_step
             self.gpu = make_gpu_step(self, use_graphs=use_graphs)
@@ -74,6 +77,8 @@ class TrainProgram:
             self.gpu.train_steps(self.batch_size, full)      # full batches come first
             for s in sizes[full:]:
                 self.gpu.train_step(s)                        # ragged tail
+            if self.sync_fn is not None:
+                self.sync_fn("training epoch")
         else:
             buf = self.metrics.buf[0:3]
             for start, size in self._bounds:
@@ -93,6 +98,8 @@ class TrainProgram:
         n = len(self.test_split)
         if self.gpu is not None:
             self.gpu.evaluate()
+            if self.sync_fn is not None:
+                self.sync_fn("evaluation")
         else:
             buf = self.metrics.buf[3:6]
             for start, size in batch_bounds(n, self.eval_batch):

@@ -27,6 +27,11 @@ def test_bench_json_contract(gpu):
     # value is the whole-job images/sec implied by the timed steps
     assert abs(d["value"] - d["config"]["global_batch"] / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
     assert d["vs_baseline"] > 1.0
+    # an epoch boundary (next epoch's sampler order: upload + gather) falls in the window
+    assert d["config"]["epoch_boundaries_timed"] >= 1
+    assert d["comm"]["world_size"] == 1
+    # N = 1: the strong-scaling (reference DDP) configuration is the same 256-image step
+    assert d["strong"]["global_batch"] == 256 and d["strong"]["batch_per_rank"] == 256
 
 
 def test_bench_transport_calibration(gpu):
@@ -42,6 +47,9 @@ def test_bench_transport_calibration(gpu):
     cal = d["config"]["transport_calibration_ms_per_step"]
     assert set(cal) == {"xgmi", "rccl"}, cal
     assert d["config"]["grad_transport"] == min(cal, key=cal.get)
+    # what the data plane saw: a 1-rank RCCL communicator, no xGMI peer to map
+    assert d["comm"]["rccl_comm_count"] == 1
+    assert d["comm"]["xgmi_peers_mapped"] == 0
 
 
 def test_bench_two_rank_flow_rehearsal(gpu):
@@ -60,6 +68,9 @@ def test_bench_two_rank_flow_rehearsal(gpu):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["global_batch"] == 2 * d["config"]["batch_per_rank"]
+    # strong scaling = the reference's split of the node batch (S:174): 128 per rank
+    assert d["strong"]["batch_per_rank"] == 128 and d["strong"]["global_batch"] == 256
+    assert d["strong"]["value"] > 0
 
 
 def test_bench_two_rank_xgmi_rehearsal(gpu):

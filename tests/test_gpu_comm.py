@@ -1,7 +1,14 @@
 """Native RCCL communicator + bucketed reducer on one GPU (1-rank communicator),
 including capture of the reducer's fork/join into a hipGraph."""
+import os
+import subprocess
+import sys
+import time
+
 import pytest
 import torch
+
+from conftest import REPO
 
 pytestmark = pytest.mark.gpu
 
@@ -91,3 +98,57 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu):
         if comm is not None:
             comm.close()
     assert torch.equal(out[0], out[1])
+
+
+def test_rccl_comm_count(gpu):
+    comm = _comm(gpu)
+    assert comm.comm_count() == 1
+    assert comm.handle.comm_user_rank() == 0
+    assert comm.handle.async_error() == 0
+    comm.close()
+
+
+_NEVER_JOINS = r"""
+import sys, time, torch
+sys.path.insert(0, sys.argv[1])
+from pytorch_distributed_mnist_amd.ops import _ext
+C = _ext.require()
+uid = C.rccl_unique_id()
+t0 = time.monotonic()
+try:
+    C.RcclComm(bytes(uid), 0, 2, 0, 4.0)      # rank 1 never calls init
+except RuntimeError as e:
+    print("RAISED %.2f %s" % (time.monotonic() - t0, e), flush=True)
+    sys.exit(0)
+print("NO ERROR", flush=True)
+sys.exit(1)
+"""
+
+
+def test_rccl_init_times_out_when_a_peer_never_joins(gpu):
+    """A 2-rank communicator whose rank 1 never arrives: rank 0 raises once the deadline
+    (--timeout, here 4 s) passes instead of hanging (non-blocking ncclCommInitRankConfig +
+    ncclCommGetAsyncError polling, csrc/runtime/comm.cpp).  Own process: the abandoned
+    communicator is aborted there."""
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", _NEVER_JOINS, REPO], capture_output=True,
+                       text=True, timeout=90)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RAISED")][0]
+    waited = float(line.split()[1])
+    assert 3.5 <= waited <= 20.0, line
+    assert "timed out" in line and "never joined" in line, line
+    assert time.monotonic() - t0 < 80
+
+
+def test_bounded_sync_aborts_and_raises(gpu):
+    """A device-side wait that outlives the deadline raises from bounded_sync."""
+    from pytorch_distributed_mnist_amd.parallel.comm import bounded_sync
+    a = torch.randn(4096, 4096, device=gpu)
+    torch.cuda.synchronize()
+    for _ in range(40):          # ~several ms of queued GEMMs, then a 1 us deadline
+        a = a @ a * 1e-3
+    with pytest.raises(RuntimeError, match="did not finish within"):
+        bounded_sync(gpu, 1e-6, None, "queued GEMMs")
+    torch.cuda.synchronize()
+    bounded_sync(gpu, 30.0, None, "idle device")      # nothing queued: returns

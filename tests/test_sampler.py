@@ -54,3 +54,13 @@ def test_batch_bounds():
     assert len(batch_bounds(60000, 256)) == 235
     assert len(batch_bounds(7500, 32)) == 235
     assert batch_bounds(10000, 256)[-1] == (9984, 16)
+
+
+def test_prefetcher_matches_direct_computation():
+    from pytorch_distributed_mnist_amd.data.sampler import EpochIndexPrefetcher, distributed_indices
+    pf = EpochIndexPrefetcher(1000, 4, 3)
+    try:
+        for e in (0, 1, 2, 5, 6):           # in order, then a jump (not prefetched)
+            assert torch.equal(pf.get(e), distributed_indices(1000, 4, 3, e))
+    finally:
+        pf.close()

@@ -1,4 +1,4 @@
-"""Per-role timing of fc1_bwd (PDM_FC1BWD_ROLE) and of the optimizer launches at B=256."""
+"""Per-role timing of fc1_bwd (PDM_FC1BWD_ROLE; needs a PDM_DIAG_ROLES=1 build via PDM_EXT_PATH) and of the optimizer launches at B=256."""
 import os
 import sys
 import torch
