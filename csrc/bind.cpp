@@ -117,7 +117,8 @@ void lin_train(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> i
 }
 
 void lin_reduce(at::Tensor slab, int64_t B, at::Tensor gW, at::Tensor gb,
-                c10::optional<at::Tensor> c0, c10::optional<at::Tensor> xg) {
+                c10::optional<at::Tensor> c0, c10::optional<at::Tensor> xg,
+                c10::optional<at::Tensor> metrics) {
   c10::DeviceGuard g(slab.device());
   need(slab, at::kFloat, "slab");
   need(gW, at::kFloat, "gW");
@@ -125,8 +126,14 @@ void lin_reduce(at::Tensor slab, int64_t B, at::Tensor gW, at::Tensor gb,
   const int64_t nblk = (B + LIN_ROWS - 1) / LIN_ROWS;
   need_numel(slab, nblk * LIN_SLAB, "slab");
   TORCH_CHECK(gW.numel() == LIN_N * LIN_K && gb.numel() == LIN_N, "bad grad views");
+  double* mp = nullptr;
+  if (metrics.has_value() && metrics->defined()) {
+    need(*metrics, at::kDouble, "metrics");
+    need_numel(*metrics, 3, "metrics");
+    mp = metrics->data_ptr<double>();
+  }
   launch_lin_reduce(slab.data_ptr<float>(), (int)nblk, gW.data_ptr<float>(), gb.data_ptr<float>(),
-                    opt_i64(c0), xg_step(xg), cur_stream(slab));
+                    opt_i64(c0), xg_step(xg), mp, cur_stream(slab));
 }
 
 void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
@@ -177,7 +184,8 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd,
                 double momentum, double dampening, bool nesterov, double grad_scale,
                 std::vector<py::tuple> segs, c10::optional<at::Tensor> xg, int64_t signal_ch,
-                std::vector<int64_t> waits, double timeout_s, c10::optional<at::Tensor> bump) {
+                std::vector<int64_t> waits, double timeout_s, c10::optional<at::Tensor> bump,
+                c10::optional<py::tuple> metrics) {
   c10::DeviceGuard dg(p.device());
   need(p, at::kFloat, "params");
   need(g, at::kFloat, "grads");
@@ -285,6 +293,25 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
   a.xg_signal_ch = (int)signal_ch;
   a.xg_timeout = (long long)(timeout_s * 1e8);
   a.bump = opt_i64(bump);
+  a.metrics = nullptr;
+  a.mslab = nullptr;
+  if (metrics.has_value()) {
+    // (slab, nslab, col, stride, metrics fp64[3]): train loss / correct partials
+    const auto& mt = *metrics;
+    TORCH_CHECK(mt.size() == 5, "metrics: (slab, nslab, col, stride, metrics)");
+    auto st = mt[0].cast<at::Tensor>();
+    auto mv = mt[4].cast<at::Tensor>();
+    need(st, at::kFloat, "metrics slab");
+    need(mv, at::kDouble, "metrics");
+    need_numel(mv, 3, "metrics");
+    a.mnslab = (int32_t)mt[1].cast<int64_t>();
+    a.mcol = (int32_t)mt[2].cast<int64_t>();
+    a.mstride = mt[3].cast<int64_t>();
+    TORCH_CHECK(a.mnslab >= 1 && a.mcol >= 0 && a.mcol + 2 <= a.mstride &&
+                    st.numel() >= (int64_t)a.mnslab * a.mstride, "metrics slab geometry");
+    a.mslab = st.data_ptr<float>();
+    a.metrics = mv.data_ptr<double>();
+  }
   TORCH_CHECK(signal_ch >= -1 && signal_ch < XG_MAX_CH, "bad signal channel");
   TORCH_CHECK(a.xg != nullptr || (signal_ch < 0 && waits.empty()),
               "optimizer waits / signals need the xgmi sync words");
@@ -320,8 +347,9 @@ void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* nam
 void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx,
              c10::optional<at::Tensor> ctr, int64_t bfull, int64_t B, at::Tensor w1, at::Tensor b1,
              at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
-             c10::optional<at::Tensor> xg, at::Tensor ylab) {
+             c10::optional<at::Tensor> xg, at::Tensor ylab, int64_t bands) {
   c10::DeviceGuard g(images.device());
+  TORCH_CHECK(bands == 1 || bands == 2 || bands == 3 || bands == 6, "bands must be 1, 2, 3 or 6");
   const bool gather = idx.has_value() && idx->defined();
   const bool counted = ctr.has_value() && ctr->defined();
   if (gather) {
@@ -358,13 +386,20 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
   need_numel(ylab, B, "ylab");
   const bool train = xg.has_value() && xg->defined();
   if (train) need_min(*xg, at::kByte, B * 784, "xg");
-  launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
-                 gather ? idx->data_ptr<int32_t>() : nullptr,
-                 gather ? idx->numel() : images.size(0), counted ? ctr->data_ptr<int64_t>() : nullptr, (int)bfull, (int)B,
-                 w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2), b2.data_ptr<float>(),
-                 ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(),
-                 train ? xg->data_ptr<uint8_t>() : nullptr, ylab.data_ptr<int32_t>(),
-                 cur_stream(images));
+  const int32_t* pidx = gather ? idx->data_ptr<int32_t>() : nullptr;
+  const int64_t nrow = gather ? idx->numel() : images.size(0);
+  const int64_t* pctr = counted ? ctr->data_ptr<int64_t>() : nullptr;
+  uint8_t* pxg = train ? xg->data_ptr<uint8_t>() : nullptr;
+  if (bands > 1)
+    launch_cnn_fwd_band(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
+                        (int)bfull, (int)B, (int)bands, w1.data_ptr<float>(), b1.data_ptr<float>(),
+                        ptr<__bf16>(w2), b2.data_ptr<float>(), ptr<__bf16>(pool),
+                        pmask.data_ptr<uint8_t>(), pxg, ylab.data_ptr<int32_t>(), cur_stream(images));
+  else
+    launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
+                   (int)bfull, (int)B, w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2),
+                   b2.data_ptr<float>(), ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(), pxg,
+                   ylab.data_ptr<int32_t>(), cur_stream(images));
 }
 
 void fc1_fwd(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_t splitk) {
@@ -484,11 +519,19 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
                  metrics.data_ptr<double>(), make_fc_update(fc_update), cur_stream(dh));
 }
 
+static int64_t conv_blocks(int64_t B, int64_t ipb, int64_t bands) {
+  return bands > 1 ? B * bands : (int64_t)cnn_bwd_blocks((int)B, (int)ipb);
+}
+
+// bands == 1: cnn_bwd (ipb images per workgroup); bands in {2, 3, 6}: cnn_bwd_band (each
+// image over `bands` workgroups; ipb must be 1)
 void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::Tensor pmask,
              at::Tensor w2t, int64_t B, int64_t ipb, at::Tensor slab,
-             c10::optional<at::Tensor> xg_sync) {
+             c10::optional<at::Tensor> xg_sync, int64_t bands) {
   c10::DeviceGuard g(xg.device());
   TORCH_CHECK(B >= 1 && ipb >= 1, "bad B/ipb");
+  TORCH_CHECK(bands == 1 || ((bands == 2 || bands == 3 || bands == 6) && ipb == 1),
+              "bands must be 1, or 2 / 3 / 6 with one image per band group");
   need_min(xg, at::kByte, B * 784, "xg");
   need(w1, at::kFloat, "w1");
   need(b1, at::kFloat, "b1");
@@ -496,10 +539,16 @@ void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::
   need_min(dpool, at::kBFloat16, B * CNN_FEAT, "dpool");
   need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
   need_min(w2t, at::kBFloat16, 288 * 64, "w2t");
-  need_min(slab, at::kFloat, (int64_t)cnn_bwd_blocks((int)B, (int)ipb) * CNN_CONV_SLAB, "conv slab");
-  launch_cnn_bwd(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
-                 ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
-                 slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
+  need_min(slab, at::kFloat, conv_blocks(B, ipb, bands) * CNN_CONV_SLAB, "conv slab");
+  need_aligned(slab.data_ptr(), 16, "conv slab");
+  if (bands > 1)
+    launch_cnn_bwd_band(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
+                        ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B,
+                        (int)bands, slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
+  else
+    launch_cnn_bwd(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
+                   ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
+                   slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
 }
 
 void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, at::Tensor gw1,
@@ -519,7 +568,7 @@ void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, 
                      cur_stream(slab));
 }
 
-int64_t cnn_bwd_nblk(int64_t B, int64_t ipb) { return cnn_bwd_blocks((int)B, (int)ipb); }
+int64_t cnn_bwd_nblk(int64_t B, int64_t ipb, int64_t bands) { return conv_blocks(B, ipb, bands); }
 
 // Upload an instantiated hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device
 // on the current stream, so its first replay inside a timed region costs the same as later ones.
@@ -535,6 +584,8 @@ at::Tensor read_stamps(const std::string& which) {
   at::Tensor t = at::zeros({256, 16}, at::TensorOptions().dtype(at::kLong));
   auto* p = reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>());
   if (which == "fwd") read_stamps_fwd(p);
+  else if (which == "fwd_band") read_stamps_fwd_band(p);
+  else if (which == "bwd_band") read_stamps_bwd_band(p);
   else read_stamps_bwd(p);
   return t;
 }
@@ -555,14 +606,15 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ctr"), py::arg("bfull"), py::arg("B"), py::arg("W"), py::arg("b"), py::arg("slab"),
         py::arg("metrics") = py::none(), py::arg("c1") = py::none());
   m.def("lin_reduce", &lin_reduce, py::arg("slab"), py::arg("B"), py::arg("gW"), py::arg("gb"),
-        py::arg("c0") = py::none(), py::arg("xg") = py::none());
+        py::arg("c0") = py::none(), py::arg("xg") = py::none(), py::arg("metrics") = py::none());
   m.def("lin_eval", &lin_eval);
   m.def("optim_step", &optim_step, py::arg("kind"), py::arg("p"), py::arg("g"), py::arg("m"),
         py::arg("v"), py::arg("lr"), py::arg("step"), py::arg("beta1"), py::arg("beta2"),
         py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"),
         py::arg("nesterov"), py::arg("grad_scale"), py::arg("segs"), py::arg("xg") = py::none(),
         py::arg("signal_ch") = -1, py::arg("waits") = std::vector<int64_t>{},
-        py::arg("timeout_s") = 60.0, py::arg("bump") = py::none());
+        py::arg("timeout_s") = 60.0, py::arg("bump") = py::none(),
+        py::arg("metrics") = py::none());
   m.def("gather_epoch", &gather_epoch);
   m.def("xgmi_wait", &xgmi_wait);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
@@ -572,7 +624,9 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CNN_CONV_SLAB_DB2") = CNN_CONV_SLAB_DB2;
   m.attr("CNN_CONV_SLAB_DW1") = CNN_CONV_SLAB_DW1;
   m.attr("CNN_CONV_SLAB_DB1") = CNN_CONV_SLAB_DB1;
-  m.def("cnn_fwd", &cnn_fwd);
+  m.def("cnn_fwd", &cnn_fwd, py::arg("images"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
+        py::arg("bfull"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
+        py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1);
   m.def("fc1_fwd", &fc1_fwd);
   m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
@@ -584,9 +638,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fc_update") = py::none());
   m.def("cnn_bwd", &cnn_bwd, py::arg("xg"), py::arg("w1"), py::arg("b1"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2t"), py::arg("B"), py::arg("ipb"), py::arg("slab"),
-        py::arg("xg_sync") = py::none());
+        py::arg("xg_sync") = py::none(), py::arg("bands") = 1);
   m.def("conv_reduce", &conv_reduce);
-  m.def("cnn_bwd_nblk", &cnn_bwd_nblk);
+  m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);
   m.def("read_stamps", &read_stamps);
   m.def("graph_upload", &graph_upload);
   register_comm(m);

@@ -113,6 +113,27 @@ __device__ __forceinline__ float4 pdm_slab_load4(const float4* p) {
   } while (0)
 #endif
 
+// One 256-thread workgroup: metrics[0] += sum_j slab[j][col], metrics[1] += sum_j
+// slab[j][col + 1] over the nslab per-workgroup slabs (row stride `stride` floats): the
+// fp32 loss / correct partials summed in fp64 in a FIXED order (thread t takes slabs t,
+// t + 128, ... of one column, then a fixed tree), so the train metrics are bitwise
+// reproducible (fp64 atomics from many workgroups are not: their order varies).
+__device__ __forceinline__ void pdm_slab_metrics(const float* __restrict__ slab, int nslab, int col,
+                                                 int64_t stride, double* __restrict__ metrics) {
+  __shared__ double red[256];
+  const int t = threadIdx.x, half = t >> 7, lt = t & 127;
+  double s = 0.0;
+  for (int j = lt; j < nslab; j += 128) s += (double)slab[(int64_t)j * stride + col + half];
+  red[t] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = 64; w > 0; w >>= 1) {
+    if (lt < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (lt == 0) metrics[half] += red[t];
+}
+
 __device__ __forceinline__ void pdm_bump_counters(int64_t* c0, int64_t* c1,
                                                   unsigned* c2 = nullptr) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -21,8 +21,10 @@ constexpr int LIN_EVAL_ROWS = 16;
 void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                       int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W, const float* b,
                       float* slab, double* metrics, int64_t* c1, hipStream_t st);
+// metrics (optional): one extra workgroup sums the loss / correct slab columns into
+// metrics[0..1] in a fixed order (lin_train only adds the sample count)
 void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, int64_t* c0, unsigned* c2,
-                       hipStream_t st);
+                       double* metrics, hipStream_t st);
 void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, const float* W,
                      const float* b, double* metrics, hipStream_t st);
 
@@ -98,6 +100,12 @@ struct OptArgs {
   // optional counter advanced once by the launch (world size 1 Linear: the data-step
   // counter, which no optimizer workgroup reads)
   int64_t* bump;
+  // optional (world size 1 Linear): one extra workgroup adds the step's train loss / correct
+  // partials (slab columns mcol, mcol + 1 of mnslab slabs) to metrics[0..1] in a fixed order
+  const float* mslab;
+  int32_t mnslab, mcol;
+  int64_t mstride;
+  double* metrics;
 };
 
 void launch_optim(int kind, OptArgs& a, hipStream_t st);
@@ -149,6 +157,12 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
                     int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
                     int32_t* ylab, hipStream_t st);
+// small batches: each image over `bands` in {2, 3, 6} workgroups of 24 / bands conv2 rows
+// (cnn_fwd_band.hip); same outputs as launch_cnn_fwd
+void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
+                         int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
+                         const float* w1, const float* b1, const __bf16* w2, const float* b2,
+                         __bf16* pool, uint8_t* pmask, uint8_t* xg, int32_t* ylab, hipStream_t st);
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st);
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
@@ -163,9 +177,16 @@ void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const _
                     const uint8_t* pmask, const __bf16* w2t, int B, int imgs_per_block, float* slab,
                     unsigned* xg_sync, hipStream_t st);
 int cnn_bwd_blocks(int B, int imgs_per_block);
+// small batches: each image split over `bands` in {2, 3, 6} workgroups of 24 / bands conv2
+// rows (cnn_bwd_band.hip); B * bands workgroups, one slab each (the cnn_bwd slab layout)
+void launch_cnn_bwd_band(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
+                         const uint8_t* pmask, const __bf16* w2t, int B, int bands, float* slab,
+                         unsigned* xg_sync, hipStream_t st);
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st);
 
 // diagnostic timestamps (all zero unless built with PDM_STAMPS=1)
 void read_stamps_fwd(unsigned long long* host);
 void read_stamps_bwd(unsigned long long* host);
+void read_stamps_fwd_band(unsigned long long* host);
+void read_stamps_bwd_band(unsigned long long* host);

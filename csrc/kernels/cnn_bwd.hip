@@ -45,15 +45,6 @@ namespace {
 
 using namespace cnn;
 
-// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1, fully expanded
-template <class F, int... Is>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
 
 #if PDM_WANT_FC1_BWD
 // ------------------------------------------------------------------ fc1_bwd

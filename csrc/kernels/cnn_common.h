@@ -3,6 +3,9 @@
 #include "../common.h"
 #include "../kernels.h"
 
+#include <type_traits>
+#include <utility>
+
 // Diagnostic build only (PDM_STAMPS=1 python -m pytorch_distributed_mnist_amd.build):
 // thread 0 of blocks 0..255 records s_memtime at phase boundaries; never in a timed build.
 #ifdef PDM_STAMPS
@@ -28,6 +31,17 @@ static __device__ unsigned long long pdm_stamps[256 * 16];
 #endif
 
 namespace cnn {
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1, fully expanded
+// (hipcc leaves long `#pragma unroll` loops rolled and keeps the arrays they index in scratch)
+template <class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 constexpr int IMG = 28;               // input 28x28
 constexpr int C1 = 32, H1 = 26, P1 = H1 * H1;   // conv1 out 26x26x32

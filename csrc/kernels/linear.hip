@@ -237,13 +237,10 @@ __global__ __launch_bounds__(THREADS) void lin_train_kernel(
     for (int r = 0; r < ROWS; ++r) { l += red[r][0]; c += red[r][1]; }
     out[N * K + N] = l;
     out[N * K + N + 1] = c;
-    // fp64 sums of fp32 partials: exact at these magnitudes, so the order of the
-    // workgroups' atomics does not change the result
-    if (metrics) {
-      atomicAdd(&metrics[0], (double)l);
-      atomicAdd(&metrics[1], (double)c);
-      if (blockIdx.x == 0) atomicAdd(&metrics[2], (double)B);
-    }
+    // loss / correct go through the slab: the launch that sums the gradient slabs (the
+    // optimizer at world size 1, lin_reduce otherwise) adds them to metrics[0..1] in a fixed
+    // order; only the sample count is added here (one writer per step)
+    if (metrics && blockIdx.x == 0) metrics[2] += (double)B;
   }
   // nothing in this launch reads the optimizer-step counter
   if (c1 && blockIdx.x == 0 && tid == 0) *c1 += 1;
@@ -252,7 +249,11 @@ __global__ __launch_bounds__(THREADS) void lin_train_kernel(
 // world size > 1: fixed-order slab sum into the gradient arena (then the all-reduce)
 __global__ __launch_bounds__(256) void lin_reduce_kernel(
     const float* __restrict__ slab, int nblk, float* __restrict__ gW, float* __restrict__ gb,
-    int64_t* c0, unsigned* c2) {
+    int64_t* c0, unsigned* c2, double* __restrict__ metrics) {
+  if (metrics != nullptr && blockIdx.x == gridDim.x - 1) {   // the train-metrics workgroup
+    pdm_slab_metrics(slab, nblk, N * K + N, LIN_SLAB, metrics);
+    return;
+  }
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < N * K + N) {
     float s = 0.f;
@@ -334,9 +335,10 @@ void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_
 }
 
 void launch_lin_reduce(const float* slab, int nblk, float* gW, float* gb, int64_t* c0,
-                       unsigned* c2, hipStream_t st) {
+                       unsigned* c2, double* metrics, hipStream_t st) {
   const int n = N * K + N;
-  lin_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(slab, nblk, gW, gb, c0, c2);
+  const int nb = (n + 255) / 256 + (metrics != nullptr ? 1 : 0);
+  lin_reduce_kernel<<<nb, 256, 0, st>>>(slab, nblk, gW, gb, c0, c2, metrics);
 }
 
 void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, const float* W,

@@ -27,6 +27,10 @@ constexpr int TR = 32, TC = 64;
 
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
+  if (a.metrics != nullptr && blockIdx.x == gridDim.x - 1) {
+    pdm_slab_metrics(a.mslab, a.mnslab, a.mcol, a.mstride, a.metrics);
+    return;
+  }
   // locate segment
   int si = 0;
 #pragma unroll 1
@@ -275,6 +279,7 @@ void launch_optim(int kind, OptArgs& a, hipStream_t st) {
     total += opt_blocks_for(a.seg[i]);
   }
   if (total == 0) return;
+  if (a.metrics != nullptr) total += 1;   // the metrics workgroup (last)
   if (kind == OPT_ADAM)
     optim_kernel<OPT_ADAM><<<total, 256, 0, st>>>(a);
   else

@@ -62,6 +62,29 @@ def choose_ipb(B: int, cus: int = 256) -> int:
     return max(1, -(-B // cus))
 
 
+BAND_CHOICES = (6, 3, 2)
+
+
+def choose_bands(B: int, cus: int = 256) -> int:
+    """Row bands per image in the conv backward: small batches (the reference's per-rank
+    split of the node batch, 256 / world_size) spread each image over up to 6 workgroups
+    (cnn_bwd_band.hip) so that B * bands fills at most one round of the CUs; 1 = cnn_bwd
+    (PDM_BANDS overrides: 1 disables the split)."""
+    forced = os.environ.get("PDM_BANDS")
+    if forced is not None:
+        return int(forced)
+    for s in BAND_CHOICES:
+        if B * s <= cus:
+            return s
+    return 1
+
+
+def conv_blocks(C, B: int) -> int:
+    """Conv-backward workgroups (= gradient slabs) for per-rank batch B."""
+    bands = choose_bands(B)
+    return C.cnn_bwd_nblk(B, choose_ipb(B) if bands == 1 else 1, bands)
+
+
 class CnnStep(GpuStepBase):
     def __init__(self, prog, use_graphs):
         super().__init__(prog, use_graphs)
@@ -85,7 +108,9 @@ class CnnStep(GpuStepBase):
                                      device=dev)
         self.dpool = torch.empty(B * 9216, dtype=bf16, device=dev)
         self.ipb = choose_ipb(B)
-        self.conv_nblk = C.cnn_bwd_nblk(B, self.ipb)
+        # slabs for every batch size this step runs (the ragged tail may split into more
+        # bands than the full batch)
+        self.conv_nblk = max(conv_blocks(C, b) for b in range(1, B + 1))
         self.conv_slab = torch.empty(self.conv_nblk * C.CNN_CONV_SLAB, dtype=torch.float32,
                                      device=dev)
         # bf16 compute copies of the weights (kept current by the optimizer kernel)
@@ -222,9 +247,10 @@ class CnnStep(GpuStepBase):
         xs = red.sync if red.streamed else None       # xgmi streamed-mode sync words
         ldt = -(-B // 32) * 32
         S = self.splitk_train
+        bands = choose_bands(B)
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                  self.pmask, self.xg, self.ylab)
+                  self.pmask, self.xg, self.ylab, bands)
         if carry_in:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(self._bucket_segments()[0])
@@ -242,16 +268,17 @@ class CnnStep(GpuStepBase):
             # bucket 0 (fc, 4.7 MB) is complete: its xGMI all-reduce kernel is small enough
             # to be co-resident with cnn_bwd, so it travels during the conv backward
             self.reducer.bucket_ready(0)
-        ipb = choose_ipb(B)
+        ipb = choose_ipb(B) if bands == 1 else 1
+        nblk = C.cnn_bwd_nblk(B, ipb, bands)
         # streamed xgmi: cnn_bwd's first workgroup publishes the fc bucket to the
         # persistent collective, which then reduces it beside cnn_bwd
         C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
-                  ipb, self.conv_slab, xs)
+                  ipb, self.conv_slab, xs, bands)
         if self.fuse_conv_reduce:
             # world_size 1: no all-reduce, the conv slab reduction runs inside the update
-            self.launch_optimizer(self._fused_segments(C.cnn_bwd_nblk(B, ipb)))
+            self.launch_optimizer(self._fused_segments(nblk))
             return
-        C.conv_reduce(self.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"], G["conv2.bias"],
+        C.conv_reduce(self.conv_slab, nblk, G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
         if xgmi and red.streamed:
             # the optimizer publishes the conv bucket; its fc workgroups wait for bucket 0

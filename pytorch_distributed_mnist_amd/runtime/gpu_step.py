@@ -165,7 +165,8 @@ class GpuStepBase:
         """[(offset, rows, cols, shadow|None, shadow_t|None)] covering the arena."""
         return [(0, 1, self.arena.spec.total, None, None)]
 
-    def launch_optimizer(self, segments=None, signal_ch: int = -1, bump=None) -> None:
+    def launch_optimizer(self, segments=None, signal_ch: int = -1, bump=None,
+                         metrics=None) -> None:
         """One fused optimizer launch over `segments` (default: every parameter).
 
         xgmi streamed mode: bucket `signal_ch` (>= 0) is published to the persistent
@@ -198,13 +199,15 @@ class GpuStepBase:
             self.C.optim_step(self.C.OPT_ADAM, self.arena.params, grads, o.exp_avg,
                               o.exp_avg_sq, o._lr_dev, o._step_dev, float(b1), float(b2),
                               float(g["eps"]), float(g["weight_decay"]), 0.0, 0.0, False,
-                              float(self.reducer.grad_scale), segs, bump=bump, **xg)
+                              float(self.reducer.grad_scale), segs, bump=bump, metrics=metrics,
+                              **xg)
         else:
             self.C.optim_step(self.C.OPT_SGD, self.arena.params, grads,
                               o.momentum_buffer, None, o._lr_dev, o._step_dev, 0.0, 0.0, 0.0,
                               float(g["weight_decay"]), float(g["momentum"]),
                               float(g["dampening"]), bool(g["nesterov"]),
-                              float(self.reducer.grad_scale), segs, bump=bump, **xg)
+                              float(self.reducer.grad_scale), segs, bump=bump, metrics=metrics,
+                              **xg)
 
     def invalidate_graphs(self) -> None:
         self.graphs.clear()
@@ -263,12 +266,15 @@ class LinearStep(GpuStepBase):
         C.lin_train(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull,
                     B, self.W, self.b, self.slab, self.metrics.train_view(), self.opt._step_dev)
         red = self.reducer
+        # the step's train loss / correct partials sit in the slabs (columns 7850, 7851): the
+        # launch that sums the gradient slabs adds them to the fp64 metrics in a fixed order
+        nblk = (B + C.LIN_ROWS - 1) // C.LIN_ROWS
+        mets = (self.slab, nblk, 10 * 784 + 10, C.LIN_SLAB, self.metrics.train_view())
         if self.fuse_reduce:
-            nblk = (B + C.LIN_ROWS - 1) // C.LIN_ROWS
-            self.launch_optimizer(self._fused_segments(nblk), bump=self.ctr[0:1])
+            self.launch_optimizer(self._fused_segments(nblk), bump=self.ctr[0:1], metrics=mets)
             return
         C.lin_reduce(self.slab, B, self.gW, self.gb, self.ctr[0:1],
-                     red.sync if red.streamed else None)
+                     red.sync if red.streamed else None, self.metrics.train_view())
         if red.streamed:
             # the optimizer publishes the bucket and waits for the persistent collective
             self.launch_optimizer(signal_ch=0)

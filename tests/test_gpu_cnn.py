@@ -39,6 +39,30 @@ def _torch_params(prog):
     return prog.arena.torch_tensors(prog.arena.params)
 
 
+@pytest.mark.parametrize("B,bands", [(5, 2), (7, 3), (4, 6), (1, 6)])
+def test_cnn_forward_band_split_bit_identical(gpu, B, bands):
+    """The small-batch row-band forward (each image over `bands` workgroups) computes the
+    same conv1 / conv2 / pool arithmetic per output as the one-workgroup-per-image kernel:
+    pooled activations, pool mask, gathered image and labels are bit-identical."""
+    prog, train, _ = _program(B)
+    st = prog.gpu
+    prog.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+    C, P = st.C, st.P
+    outs = []
+    for b in (1, bands):
+        for t in (st.pool, st.pmask, st.xg, st.ylab):
+            t.fill_(0x55 if t.dtype == torch.uint8 else 7)
+        C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, st.ctr[0:1], st.bfull, B,
+                  P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"], st.pool, st.pmask,
+                  st.xg, st.ylab, b)
+        torch.cuda.synchronize()
+        outs.append([st.pool[:B * 9216].clone(), st.pmask[:B * 9216].clone(),
+                     st.xg[:B * 784].clone(), st.ylab[:B].clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.uint8) if a.dtype == torch.bfloat16 else a,
+                           b.view(torch.uint8) if b.dtype == torch.bfloat16 else b)
+
+
 @pytest.mark.parametrize("B", [64, 37])
 def test_cnn_forward_kernels(gpu, B):
     prog, train, _ = _program(B)

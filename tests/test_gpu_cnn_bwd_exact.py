@@ -19,8 +19,11 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("B,ipb", [(3, 1), (5, 2), (7, 3)])
-def test_cnn_bwd_exact(gpu, B, ipb):
+@pytest.mark.parametrize("B,ipb,bands", [(3, 1, 1), (5, 2, 1), (7, 3, 1),
+                                         (3, 1, 2), (5, 1, 3), (4, 1, 6), (1, 1, 6)])
+def test_cnn_bwd_exact(gpu, B, ipb, bands):
+    """cnn_bwd (bands = 1, ipb images per workgroup) and the small-batch row-band split
+    cnn_bwd_band (each image over `bands` workgroups) against fp64."""
     C = _C()
     g = torch.Generator().manual_seed(B)
     xg = torch.randint(0, 256, (B, 784), generator=g, dtype=torch.uint8)
@@ -37,10 +40,11 @@ def test_cnn_bwd_exact(gpu, B, ipb):
     pmask = torch.where(pos, 0x80 | (1 << s), 0).to(torch.uint8)   # cnn_fwd's encoding
     w2 = torch.randn(64, 9, 32, generator=g).to(torch.bfloat16)          # [co][tap][ci]
     w2t = w2.reshape(64, 288).t().contiguous()                             # [tap*32+ci][co]
-    nblk = C.cnn_bwd_nblk(B, ipb)
-    slab = torch.zeros(nblk * C.CNN_CONV_SLAB, device=gpu)
+    nblk = C.cnn_bwd_nblk(B, ipb, bands)
+    assert nblk == (B * bands if bands > 1 else -(-B // ipb))
+    slab = torch.full((nblk * C.CNN_CONV_SLAB,), float("nan"), device=gpu)   # every entry written
     C.cnn_bwd(xg.to(gpu), w1.to(gpu), b1.to(gpu), dpool.to(gpu), pmask.to(gpu), w2t.to(gpu), B,
-              ipb, slab)
+              ipb, slab, None, bands)
     gw2 = torch.zeros(64 * 288, device=gpu)
     gb2 = torch.zeros(64, device=gpu)
     gw1 = torch.zeros(288, device=gpu)

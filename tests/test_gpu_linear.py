@@ -45,7 +45,8 @@ def test_lin_train_reduce_matches_torch(gpu, B, bfull, gather):
     else:             # epoch buffer: rows ctr * bfull + i of the gathered epoch
         C.lin_train(images[idx.long()].to(dev), labels[idx.long()].to(dev, torch.int32), None,
                     ctr[0:1], bfull, B, W.to(dev), b.to(dev), slab, metrics, ostep)
-    C.lin_reduce(slab, B, gW, gb, ctr[0:1])
+    # lin_reduce also adds the train loss / correct partials (fixed order) to the metrics
+    C.lin_reduce(slab, B, gW, gb, ctr[0:1], None, metrics)
     torch.cuda.synchronize()
     assert torch.allclose(gW.cpu(), Wr.grad, atol=2e-6, rtol=1e-4)
     assert torch.allclose(gb.cpu(), br.grad, atol=2e-6, rtol=1e-4)
@@ -120,3 +121,20 @@ def test_linear_fused_reduce_matches_unfused(gpu, opt, monkeypatch):
     assert (a[0] - b[0]).abs().max().item() < 1e-6
     assert abs(a[1] - b[1]) < 1e-6 and a[2] == b[2]   # slab sums in a different order
     assert a[3] == b[3] == 9 and a[4] == b[4] == 9
+
+
+def test_linear_train_metrics_bitwise_reproducible(gpu):
+    """Two identical epochs give bit-identical fp64 train loss sums (fixed-order reduction of
+    the per-workgroup partials, no fp64 atomics)."""
+    train = synthetic_split(256 * 6, True)
+    test = synthetic_split(64, False)
+    out = []
+    for _ in range(2):
+        p = build_local_program("linear", "fp32", "cuda", 256, train, test, optimizer="adam",
+                                lr=1e-3, seed=3, use_graphs=True)
+        p.optimizer.sync_hyperparams()
+        p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        p.train_epoch()
+        torch.cuda.synchronize()
+        out.append(p.metrics.buf[0:3].clone())
+    assert torch.equal(out[0], out[1]), out

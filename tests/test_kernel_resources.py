@@ -43,7 +43,7 @@ def test_no_kernel_uses_scratch(kernels):
 def test_every_hot_kernel_is_present(kernels):
     for name in ("cnn_fwd_kernel", "fc1_fwd_kernel", "cnn_head_kernel", "fc1_bwd_kernel",
                  "cnn_bwd_kernel", "conv_reduce_kernel", "optim_kernel", "lin_train_kernel",
-                 "xgmi_allreduce_kernel"):
+                 "xgmi_allreduce_kernel", "cnn_fwd_band_kernel", "cnn_bwd_band_kernel"):
         _find(kernels, name)
 
 
@@ -56,6 +56,14 @@ def test_occupancy_budgets(kernels):
     for k, v in _find(kernels, "cnn_fwd_kernel").items():
         assert v["group_segment_fixed_size"] <= 81920, k
         assert v["vgpr_count"] + v.get("agpr_count", 0) <= 128, k
+    # small-batch row-band kernels: cnn_fwd_band two 512-thread workgroups per CU,
+    # cnn_bwd_band one (<= 256 registers per lane), both within the 160 KB LDS
+    for k, v in _find(kernels, "cnn_fwd_band_kernel").items():
+        assert v["group_segment_fixed_size"] <= 81920, k
+        assert v["vgpr_count"] + v.get("agpr_count", 0) <= 128, k
+    for k, v in _find(kernels, "cnn_bwd_band_kernel").items():
+        assert v["group_segment_fixed_size"] <= 163840, k
+        assert v["vgpr_count"] + v.get("agpr_count", 0) <= 256, k
     # fc1_bwd: 256 threads, one wave per SIMD per workgroup, all roles one round
     for k, v in _find(kernels, "fc1_bwd_kernel").items():
         assert v["vgpr_count"] + v.get("agpr_count", 0) <= 512, k

@@ -5,7 +5,7 @@ sys.path.insert(0, ".")
 from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
 from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
 from pytorch_distributed_mnist_amd.runtime.program import build_local_program
-from pytorch_distributed_mnist_amd.runtime.cnn_step import choose_ipb
+from pytorch_distributed_mnist_amd.runtime.cnn_step import choose_bands, choose_ipb
 
 train = synthetic_split(60000, True)
 test = synthetic_split(512, False)
@@ -46,7 +46,9 @@ def main():
       C, P, G = st.C, st.P, st.G
       ldt = -(-B // 32) * 32
       S = st.splitk_train
-      ipb = choose_ipb(B)
+      bands = choose_bands(B)
+      ipb = choose_ipb(B) if bands == 1 else 1
+      nblk = C.cnn_bwd_nblk(B, ipb, bands)
       st.train_step(B)
       torch.cuda.synchronize()
       z = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -63,11 +65,11 @@ def main():
                                        G["fc1.bias"], st.metrics.train_view(),
                                        st._fc_update() if st.fuse_fc1 else None),
           "cnn_bwd": lambda: C.cnn_bwd(st.xg, P["conv1.weight"], P["conv1.bias"], st.dpool, st.pmask,
-                                       st.w2t, B, ipb, st.conv_slab),
-          "conv_reduce": lambda: C.conv_reduce(st.conv_slab, C.cnn_bwd_nblk(B, ipb), G["conv2.weight"],
+                                       st.w2t, B, ipb, st.conv_slab, None, bands),
+          "conv_reduce": lambda: C.conv_reduce(st.conv_slab, nblk, G["conv2.weight"],
                                                G["conv2.bias"], G["conv1.weight"], G["conv1.bias"]),
           # the training step's update: the slab-fused launch at world size 1
-          "optim": (lambda: st.launch_optimizer(st._fused_segments(C.cnn_bwd_nblk(B, ipb))))
+          "optim": (lambda: st.launch_optimizer(st._fused_segments(nblk)))
                    if st.fuse_conv_reduce else (lambda: st.launch_optimizer()),
       }
       tot = 0.0
@@ -78,7 +80,7 @@ def main():
           line.append(f"{name}={us:.1f}")
       st.ctr.zero_()   # each step advances the data counter (rows are clamped past the epoch)
       step = timeit(lambda: st._train_impl(B), 8)
-      print(f"B={B:5d} S={S} ipb={ipb} " + " ".join(line) + f" | sum={tot:.1f}us step={step:.1f}us "
+      print(f"B={B:5d} S={S} ipb={ipb} bands={bands} " + " ".join(line) + f" | sum={tot:.1f}us step={step:.1f}us "
             f"-> {B / step * 1e6 / 1e6:.2f}M img/s", flush=True)
 
 

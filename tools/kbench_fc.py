@@ -6,7 +6,7 @@ sys.path.insert(0, ".")
 from pytorch_distributed_mnist_amd.data.mnist import synthetic_split  # noqa: E402
 from pytorch_distributed_mnist_amd.data.sampler import distributed_indices  # noqa: E402
 from pytorch_distributed_mnist_amd.runtime.program import build_local_program  # noqa: E402
-from pytorch_distributed_mnist_amd.runtime.cnn_step import choose_ipb  # noqa: E402
+from pytorch_distributed_mnist_amd.runtime.cnn_step import conv_blocks  # noqa: E402
 sys.path.insert(0, "tools")
 from kbench import timeit  # noqa: E402
 
@@ -28,6 +28,6 @@ us = timeit(lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.we
                               st._fc_update() if st.fuse_fc1 else None))
 print(f"B={B} fc1_bwd role={role}: {us:.2f} us", flush=True)
 if role == "all":
-    nb = C.cnn_bwd_nblk(B, choose_ipb(B))
+    nb = conv_blocks(C, B)
     print(f"optim fused: {timeit(lambda: st.launch_optimizer(st._fused_segments(nb))):.2f} us  "
           f"plain: {timeit(lambda: st.launch_optimizer()):.2f} us", flush=True)
