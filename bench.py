@@ -175,18 +175,30 @@ def main():
             torch.cuda.synchronize()
             return allmax(time.perf_counter() - t0)
 
-        def use(red):
+        def use(red, carry=True):
             prog.reducer = red
             prog.gpu.reducer = red
             prog.gpu.use_graphs = bool(a.graphs) and red.capturable
+            if hasattr(prog.gpu, "fc_carry"):
+                prog.gpu.fc_carry = carry
             prog.gpu.invalidate_graphs()
+
+        # candidate step structures: every transport, and for RCCL the fc-update carry on/off
+        # (cnn_step.CnnStep.fc_carry) unless PDM_FC_CARRY forces it
+        cands = []
+        for name, red in reducers.items():
+            if name == "rccl" and model == "cnn" and os.environ.get("PDM_FC_CARRY") is None:
+                cands += [("rccl", red, True), ("rccl-nocarry", red, False)]
+            else:
+                cands.append((name, red, os.environ.get("PDM_FC_CARRY", "1") != "0"))
 
         opt.sync_hyperparams()
         next_epoch()
         calib = {}
-        if len(reducers) > 1:
-            for name, red in reducers.items():
-                use(red)
+        if len(cands) > 1:
+            for name, red, carry in cands:
+                use(red, carry)
+                prog.gpu.prepare(B)            # capture outside the calibration window
                 run(16)
                 calib[name] = timed(48) / 48 * 1e3
                 try:
@@ -202,7 +214,7 @@ def main():
                     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
                     ok = int(t.item())
                 if not ok:
-                    if name == "rccl":
+                    if name.startswith("rccl"):
                         raise RuntimeError("rccl transport failed calibration")
                     del calib[name]
                     sync("recovery")
@@ -212,9 +224,11 @@ def main():
                     if hasattr(prog.gpu, "refresh_shadows"):
                         prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
             best = min(calib, key=calib.get)
-            use(reducers[best])
+            _, red, carry = next(c for c in cands if c[0] == best)
+            use(red, carry)
         else:
-            use(first)
+            use(cands[0][1], cands[0][2])
+            best = cands[0][0]
         chosen = prog.reducer
         # capture + upload the step graphs outside the timed window (a graph captured lazily
         # on first use would put its capture inside a short timed run)
@@ -237,7 +251,7 @@ def main():
             raise RuntimeError("non-finite parameters after the benchmark")
         ms = elapsed / a.steps * 1e3
         return {"B": B, "global_batch": B * ws, "elapsed": elapsed, "ms": ms,
-                "value": a.steps * B * ws / elapsed, "transport": chosen.kind,
+                "value": a.steps * B * ws / elapsed, "transport": best,
                 "calib": {k: round(v, 5) for k, v in calib.items()},
                 "graphs": bool(prog.gpu.use_graphs), "epoch_boundaries_timed": boundaries}
 

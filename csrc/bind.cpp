@@ -347,7 +347,8 @@ void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* nam
 void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx,
              c10::optional<at::Tensor> ctr, int64_t bfull, int64_t B, at::Tensor w1, at::Tensor b1,
              at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
-             c10::optional<at::Tensor> xg, at::Tensor ylab, int64_t bands) {
+             c10::optional<at::Tensor> xg, at::Tensor ylab, int64_t bands,
+             c10::optional<at::Tensor> a1g, c10::optional<at::Tensor> xng) {
   c10::DeviceGuard g(images.device());
   TORCH_CHECK(bands == 1 || bands == 2 || bands == 3 || bands == 6, "bands must be 1, 2, 3 or 6");
   const bool gather = idx.has_value() && idx->defined();
@@ -390,16 +391,30 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
   const int64_t nrow = gather ? idx->numel() : images.size(0);
   const int64_t* pctr = counted ? ctr->data_ptr<int64_t>() : nullptr;
   uint8_t* pxg = train ? xg->data_ptr<uint8_t>() : nullptr;
-  if (bands > 1)
+  if (bands > 1) {
+    // training: the band backward's inputs (a1 image + normalised x) instead of the uint8 x
+    __bf16* pa1 = nullptr;
+    __bf16* pxn = nullptr;
+    if (train) {
+      TORCH_CHECK(a1g.has_value() && xng.has_value(), "band training needs a1g and xng");
+      need_min(*a1g, at::kBFloat16, B * 676 * 32, "a1g");
+      need_min(*xng, at::kBFloat16, B * 784, "xng");
+      need_aligned(a1g->data_ptr(), 16, "a1g");
+      need_aligned(xng->data_ptr(), 16, "xng");
+      pa1 = ptr<__bf16>(*a1g);
+      pxn = ptr<__bf16>(*xng);
+    }
     launch_cnn_fwd_band(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
                         (int)bfull, (int)B, (int)bands, w1.data_ptr<float>(), b1.data_ptr<float>(),
                         ptr<__bf16>(w2), b2.data_ptr<float>(), ptr<__bf16>(pool),
-                        pmask.data_ptr<uint8_t>(), pxg, ylab.data_ptr<int32_t>(), cur_stream(images));
-  else
+                        pmask.data_ptr<uint8_t>(), pa1, pxn, ylab.data_ptr<int32_t>(),
+                        cur_stream(images));
+  } else {
     launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
                    (int)bfull, (int)B, w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2),
                    b2.data_ptr<float>(), ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(), pxg,
                    ylab.data_ptr<int32_t>(), cur_stream(images));
+  }
 }
 
 void fc1_fwd(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_t splitk) {
@@ -527,7 +542,8 @@ static int64_t conv_blocks(int64_t B, int64_t ipb, int64_t bands) {
 // image over `bands` workgroups; ipb must be 1)
 void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::Tensor pmask,
              at::Tensor w2t, int64_t B, int64_t ipb, at::Tensor slab,
-             c10::optional<at::Tensor> xg_sync, int64_t bands) {
+             c10::optional<at::Tensor> xg_sync, int64_t bands, c10::optional<at::Tensor> a1g,
+             c10::optional<at::Tensor> xng) {
   c10::DeviceGuard g(xg.device());
   TORCH_CHECK(B >= 1 && ipb >= 1, "bad B/ipb");
   TORCH_CHECK(bands == 1 || ((bands == 2 || bands == 3 || bands == 6) && ipb == 1),
@@ -541,11 +557,16 @@ void cnn_bwd(at::Tensor xg, at::Tensor w1, at::Tensor b1, at::Tensor dpool, at::
   need_min(w2t, at::kBFloat16, 288 * 64, "w2t");
   need_min(slab, at::kFloat, conv_blocks(B, ipb, bands) * CNN_CONV_SLAB, "conv slab");
   need_aligned(slab.data_ptr(), 16, "conv slab");
-  if (bands > 1)
-    launch_cnn_bwd_band(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
-                        ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B,
-                        (int)bands, slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
-  else
+  if (bands > 1) {
+    TORCH_CHECK(a1g.has_value() && xng.has_value(), "the band backward needs a1g and xng");
+    need_min(*a1g, at::kBFloat16, B * 676 * 32, "a1g");
+    need_min(*xng, at::kBFloat16, B * 784, "xng");
+    need_aligned(a1g->data_ptr(), 16, "a1g");
+    need_aligned(xng->data_ptr(), 16, "xng");
+    launch_cnn_bwd_band(ptr<__bf16>(*a1g), ptr<__bf16>(*xng), ptr<__bf16>(dpool),
+                        pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)bands,
+                        slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
+  } else
     launch_cnn_bwd(xg.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
                    ptr<__bf16>(dpool), pmask.data_ptr<uint8_t>(), ptr<__bf16>(w2t), (int)B, (int)ipb,
                    slab.data_ptr<float>(), opt_sync(xg_sync), cur_stream(xg));
@@ -626,7 +647,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CNN_CONV_SLAB_DB1") = CNN_CONV_SLAB_DB1;
   m.def("cnn_fwd", &cnn_fwd, py::arg("images"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
         py::arg("bfull"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
-        py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1);
+        py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1,
+        py::arg("a1g") = py::none(), py::arg("xng") = py::none());
   m.def("fc1_fwd", &fc1_fwd);
   m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
@@ -638,7 +660,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fc_update") = py::none());
   m.def("cnn_bwd", &cnn_bwd, py::arg("xg"), py::arg("w1"), py::arg("b1"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2t"), py::arg("B"), py::arg("ipb"), py::arg("slab"),
-        py::arg("xg_sync") = py::none(), py::arg("bands") = 1);
+        py::arg("xg_sync") = py::none(), py::arg("bands") = 1, py::arg("a1g") = py::none(),
+        py::arg("xng") = py::none());
   m.def("conv_reduce", &conv_reduce);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);
   m.def("read_stamps", &read_stamps);

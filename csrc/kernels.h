@@ -158,11 +158,13 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
                     int32_t* ylab, hipStream_t st);
 // small batches: each image over `bands` in {2, 3, 6} workgroups of 24 / bands conv2 rows
-// (cnn_fwd_band.hip); same outputs as launch_cnn_fwd
+// (cnn_fwd_band.hip); same pool / pmask / ylab as launch_cnn_fwd; training (a1g != null) also
+// writes the a1 image and the normalised x for cnn_bwd_band instead of the uint8 x
 void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                          int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
-                         __bf16* pool, uint8_t* pmask, uint8_t* xg, int32_t* ylab, hipStream_t st);
+                         __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, int32_t* ylab,
+                         hipStream_t st);
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st);
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
@@ -178,8 +180,10 @@ void launch_cnn_bwd(const uint8_t* xg, const float* w1, const float* b1, const _
                     unsigned* xg_sync, hipStream_t st);
 int cnn_bwd_blocks(int B, int imgs_per_block);
 // small batches: each image split over `bands` in {2, 3, 6} workgroups of 24 / bands conv2
-// rows (cnn_bwd_band.hip); B * bands workgroups, one slab each (the cnn_bwd slab layout)
-void launch_cnn_bwd_band(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
+// rows (cnn_bwd_band.hip); B * bands workgroups, one slab each (the cnn_bwd slab layout).
+// Reads the a1 image (swizzled, [B][26*26*32]) and the normalised x ([B][784] bf16) that
+// cnn_fwd_band wrote, instead of recomputing conv1.
+void launch_cnn_bwd_band(const __bf16* a1g, const __bf16* xng, const __bf16* dpool,
                          const uint8_t* pmask, const __bf16* w2t, int B, int bands, float* slab,
                          unsigned* xg_sync, hipStream_t st);
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,

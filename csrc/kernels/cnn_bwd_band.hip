@@ -7,7 +7,7 @@
 // conv2-output (dz2) rows [d0, d0 + R) and the conv1-output (a1) rows [d0, d0 + R) (the last
 // band also rows 24, 25), so an image's work is spread over S CUs:
 //
-//   staging   x rows [d0, d0 + R + 4) -> LUT normalise -> conv1 recompute of a1 rows
+//   staging   x rows [d0, d0 + R + 4) -> normalise -> conv1 recompute of a1 rows
 //             [d0, d0 + R + 2) (MFMA 16x16x16 on the 28-wide virtual grid, as cnn_bwd);
 //             dz2 = maxpool^-1(dpool) for dz2 rows [d0 - 2, d0 + R + 2) (the 2-row halo above
 //             feeds the dgrad of the band's first a1 rows; halo rows outside the image and the
@@ -39,19 +39,20 @@ struct BandLds {
   static constexpr int AR = R + 2;              // a1 rows recomputed
   static constexpr int ZR = R + 5;              // dz2 rows staged: global [d0 - 2, d0 + R + 3)
   static constexpr int XS = 0;                  // bf16 [XR * 28 + 16]
-  static constexpr int A1 = ((XR * IMG + 16) * 2 + 127) / 128 * 128;
+  static constexpr int A1 = ((XR * IMG + 16) * 2 + 1023) / 1024 * 1024;   // (DMA pieces of 1 KB)
   static constexpr int Z0 = A1 + AR * H1 * 64;  // 4 zero pixels: column -1, -2 of dz2 row 0
   static constexpr int DZ = Z0 + 512;
   static constexpr int W2 = DZ + ZR * DSB * 128;
-  static constexpr int LUT = W2 + 9 * C1 * C2 * 2;
-  static constexpr int SPARE = LUT + 512;       // target of dropped conv1 stores
-  static constexpr int TOTAL = SPARE + 512;
+  static constexpr int TOTAL = W2 + 9 * C1 * C2 * 2;
   static constexpr int RED = DZ;                // reduction scratch (dz2 is dead by then)
   static constexpr int KS = 3 * R / 4;          // wgrad k-steps
-  static constexpr int NT1 = (AR * IMG + 15) / 16;   // conv1 tiles (16 virtual pixels)
-  static constexpr int TPW1 = (NT1 + 7) / 8;
   static constexpr int PR = R / 2 + 1;          // pooled rows staged (own + 1 above)
-  static constexpr int NIT = (PR * HP * 8 + BTH - 1) / BTH;   // scatter items per thread
+  static constexpr int SCT = 192;               // scatter threads (waves 5-7)
+  static constexpr int NIT = (PR * HP * 8 + SCT - 1) / SCT;   // scatter items per thread
+  // dgrad tiles per dgrad wave (waves 4-7 take tiles wd + 4 k, k < MD, in one pass; the wgrad
+  // waves take the band's remaining tiles after their wgrad): balances wgrad's 15 R MFMAs
+  // per wave against dgrad's 36 per tile
+  static constexpr int MD = R == 4 ? 2 : (R == 8 ? 4 : 5);
   static_assert(TOTAL <= 163840, "band LDS carve");
   static_assert(A1 % 128 == 0 && DZ % 128 == 0 && W2 % 128 == 0, "128-B aligned images");
   static_assert((8 * C2 + 4 * C1 * 16) * 4 <= ZR * DSB * 128, "reduction scratch fits dz2");
@@ -157,9 +158,9 @@ __device__ __forceinline__ void band_dgrad(const char* smem, int tile0, int aown
 
 template <int R>
 __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
-    const uint8_t* __restrict__ xg, const float* __restrict__ w1, const float* __restrict__ b1,
-    const bf16* __restrict__ dpool, const uint8_t* __restrict__ pmask,
-    const bf16* __restrict__ w2t, float* __restrict__ slab, unsigned* xg_sync) {
+    const bf16* __restrict__ a1g, const bf16* __restrict__ xng, const bf16* __restrict__ dpool,
+    const uint8_t* __restrict__ pmask, const bf16* __restrict__ w2t, float* __restrict__ slab,
+    unsigned* xg_sync) {
   using L = BandLds<R>;
   constexpr int S = L::S;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
@@ -175,55 +176,52 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
   const int npr = d0 / 2 + R / 2 - pr0;          // staged pooled rows
   const int pown0 = d0 / 2;                      // first own pooled row
   bf16* xs = reinterpret_cast<bf16*>(smem + L::XS);
-  bf16* lut = reinterpret_cast<bf16*>(smem + L::LUT);
   float* out = slab + (int64_t)blockIdx.x * CNN_CONV_SLAB;
   PDM_STAMP(0);
 
-  // ---- 1. loads (vmcnt retires in order: x and the conv1 weights first)
-  uint32_t xw = 0;
-  if (tid < L::XR * 7) xw = reinterpret_cast<const uint32_t*>(xg + (int64_t)img * 784)[d0 * 7 + tid];
-  float w1v[2][4];
-  int toff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tap = 4 * g + j;
-    toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : 0;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) w1v[mt][j] = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
-  }
-  f32x4 b1v[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  // ---- 1. loads, split by role (vmcnt is per wave: the scatter waves never wait for a DMA)
+  //   waves 0-1   a1 rows [d0, d0 + R + 2) as the forward left them (its swizzled LDS image,
+  //               cnn_fwd_band) and the normalised x rows [d0, d0 + R + 4), by LDS-DMA
+  //   waves 2-4   W2^T (36 KB) by LDS-DMA
+  //   waves 5-7   dpool / pmask items of the staged pooled rows
   const int nit = npr * HP * 8;
-  const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT) + pr0 * HP * 8;
-  const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT) + pr0 * HP * 8;
   uint4 d[L::NIT];
   uint2 mk[L::NIT];
+  if (wave < 2) {
+    constexpr int AB = L::AR * H1 * 64;          // a1 bytes
+    constexpr int NA = (AB + 1023) / 1024;       // 1-KB DMA pieces
+    const char* asrc = reinterpret_cast<const char*>(a1g + (int64_t)img * (P1 * C1) + d0 * H1 * C1);
+    const unsigned abase = lds_addr(smem) + L::A1;
 #pragma unroll
-  for (int k = 0; k < L::NIT; ++k) {
-    const int it = min(tid + k * BTH, nit - 1);
-    d[k] = dpv[it];
-    mk[k] = mkv[it];
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  {
+    for (int m = 0; m < (NA + 1) / 2; ++m) {
+      const int blk = wave + 2 * m;
+      if (blk < NA && blk * 1024 + lane * 16 < AB) glds16(asrc + blk * 1024 + lane * 16, abase + blk * 1024);
+    }
+    if (wave == 1 && lane * 16 < L::XR * IMG * 2)    // x rows: XR * 56 B <= 1 KB
+      glds16(reinterpret_cast<const char*>(xng + (int64_t)img * 784 + d0 * IMG) + lane * 16,
+             lds_addr(smem) + L::XS);
+  } else if (wave < 5) {
     const unsigned wbase = lds_addr(smem) + L::W2;
 #pragma unroll
-    for (int m = 0; m < (W2_CHUNKS / 64 + 7) / 8; ++m) {
-      const int blk = wave + 8 * m;
-      if (blk < W2_CHUNKS / 64) {
-        const int row = 8 * blk + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
-        glds16(w2t + row * 64 + ch * 8, wbase + blk * 1024);
-      }
+    for (int m = 0; m < W2_CHUNKS / 64 / 3; ++m) {
+      const int blk = (wave - 2) + 3 * m;
+      const int row = 8 * blk + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
+      glds16(w2t + row * 64 + ch * 8, wbase + blk * 1024);
+    }
+  } else {
+    const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT) + pr0 * HP * 8;
+    const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT) + pr0 * HP * 8;
+#pragma unroll
+    for (int k = 0; k < L::NIT; ++k) {
+      const int it = min(tid - 320 + k * L::SCT, nit - 1);
+      d[k] = dpv[it];
+      mk[k] = mkv[it];
     }
   }
   __builtin_amdgcn_sched_barrier(0);
   PDM_STAMP(1);
-  // ---- 2. LUT + zero fills: the 2 pad columns of every staged dz2 row, the rows the
-  // scatter does not write (halo rows outside the image, overflow rows), the zero block
-  if (tid >= 256) lut[tid - 256] = to_bf16(pdm_normalize(tid - 256));
+  // ---- 2. zero fills: the 2 pad columns of every staged dz2 row, the rows the scatter does
+  // not write (halo rows outside the image, overflow rows), the zero block, the x pad
   {
     const int zlo = 2 * pr0 - (d0 - 2);          // first scattered local row (0 or 2)
     const int zhi = zlo + 2 * npr;               // = R + 2
@@ -240,56 +238,17 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
       }
       *reinterpret_cast<uint4*>(smem + off + ch * 16) = make_uint4(0, 0, 0, 0);
     }
+    if (tid < 2) reinterpret_cast<uint4*>(xs + L::XR * IMG)[tid] = make_uint4(0, 0, 0, 0);
   }
-  __syncthreads();   // LUT ready
   PDM_STAMP(2);
-  // ---- 3. x through the LUT, conv1 recompute of a1 rows [d0, d0 + R + 2)
-  if (tid < L::XR * 7) {
-    bf16x4 v = {lut[xw & 0xff], lut[(xw >> 8) & 0xff], lut[(xw >> 16) & 0xff], lut[xw >> 24]};
-    reinterpret_cast<bf16x4*>(xs)[tid] = v;
-  } else if (tid < L::XR * 7 + 4) {
-    reinterpret_cast<bf16x4*>(xs)[tid] = bf16x4{};
-  }
-  bf16x4 w1f[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
-  __syncthreads();
-  {
-    const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);
-    bf16x4 bx[L::TPW1];
-    int vv[L::TPW1];
-#pragma unroll
-    for (int k = 0; k < L::TPW1; ++k) {
-      vv[k] = (wave + 8 * k) * 16 + i16;
-      const int vc = min(vv[k], L::AR * IMG - 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bx[k][j] = xs[vc + toff[j]];
-    }
-#pragma unroll
-    for (int k = 0; k < L::TPW1; ++k) {
-      const int y = vv[k] / IMG, x = vv[k] - y * IMG;
-      const bool ok = y < L::AR && x < H1;
-      const int ab = (vv[k] - 2 * y) * 64 + a1c;
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-        bf16x4 o = {to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
-                    to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
-        const int dst = ok ? L::A1 + (ab ^ (32 * mt)) : L::SPARE + lane * 8;
-        *reinterpret_cast<bf16x4*>(smem + dst) = o;
-      }
-    }
-  }
   PDM_STAMP(3);
   // ---- 4. the dz2 scatter of pooled rows [pr0, pr0 + npr) (+ the conv2 bias gradient of the
   // band's own pooled rows), whole-window writes as in cnn_bwd
   float db2p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < L::NIT; ++k) {
-    const int it = tid + k * BTH;   // it & 7 == tid & 7: fixed channel chunk
-    if (it < nit) {
+    const int it = tid - 320 + k * L::SCT;   // it & 7 == tid & 7: fixed channel chunk
+    if (wave >= 5 && it < nit) {
       const int pl = it >> 3, ch = it & 7;
       const int pyl = pl / HP, px = pl - pyl * HP;
       const int py = pr0 + pyl;
@@ -329,7 +288,7 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
     }
   }
   PDM_STAMP(4);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the W2^T DMA has landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA pieces have landed
   __syncthreads();
   PDM_STAMP(5);
 
@@ -422,24 +381,32 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
           pdm_slab_store(&out[o + (mt * 16 + r) * 288 + tap * 32 + nt * 16], acc[pi][mt][r]);
     }
     PDM_STAMP(6);
-  } else {
-    // ===== conv2 dgrad over the band's own a1 rows, tiles wd + 4 j =====
-    const int wd = wave - 4;
+    // then the band's dgrad tiles past the dgrad waves' 4 MD (last band / R = 12)
     const int ntile = (aown * IMG + 15) / 16;
-    constexpr int MTP = 4;
 #pragma unroll 1
-    for (int t0 = wd; t0 < ntile; t0 += 4 * MTP) band_dgrad<R, MTP, 2>(smem, t0, aown, ka1, acc1);
+    for (int t = 4 * L::MD + wave; t < ntile; t += 4) band_dgrad<R, 1, 2>(smem, t, aown, ka1, acc1);
+  } else {
+    // ===== conv2 dgrad over the band's own a1 rows: tiles wd + 4 k, k < MD =====
+    band_dgrad<R, L::MD, 2>(smem, wave - 4, aown, ka1, acc1);
     if (tid == 256) PDM_STAMP_VAL(7, PDM_CLOCK());
   }
   __syncthreads();   // every wave is done with the dz2 / a1 images (RED aliases dz2)
   PDM_STAMP(8);
   float* red = reinterpret_cast<float*>(smem + L::RED);
+  // conv1 weight/bias partials: waves 4-7 write slot wave & 3, waves 0-3 add theirs
+  float* r1 = red + RED_DW1 + (wave & 3) * C1 * 16;
   if (wave >= 4) {
-    float* r1 = red + RED_DW1 + (wave & 3) * C1 * 16;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) r1[(nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) r1[(nt * 16 + 4 * g + r) * 16 + i16] += acc1[nt][r];
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -464,19 +431,19 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
 
 }  // namespace
 
-void launch_cnn_bwd_band(const uint8_t* xg, const float* w1, const float* b1, const __bf16* dpool,
+void launch_cnn_bwd_band(const __bf16* a1g, const __bf16* xng, const __bf16* dpool,
                          const uint8_t* pmask, const __bf16* w2t, int B, int bands, float* slab,
                          unsigned* xg_sync, hipStream_t st) {
   const int nblk = B * bands;
   switch (bands) {
     case 2:
-      cnn_bwd_band_kernel<12><<<nblk, BTH, 0, st>>>(xg, w1, b1, dpool, pmask, w2t, slab, xg_sync);
+      cnn_bwd_band_kernel<12><<<nblk, BTH, 0, st>>>(a1g, xng, dpool, pmask, w2t, slab, xg_sync);
       break;
     case 3:
-      cnn_bwd_band_kernel<8><<<nblk, BTH, 0, st>>>(xg, w1, b1, dpool, pmask, w2t, slab, xg_sync);
+      cnn_bwd_band_kernel<8><<<nblk, BTH, 0, st>>>(a1g, xng, dpool, pmask, w2t, slab, xg_sync);
       break;
     case 6:
-      cnn_bwd_band_kernel<4><<<nblk, BTH, 0, st>>>(xg, w1, b1, dpool, pmask, w2t, slab, xg_sync);
+      cnn_bwd_band_kernel<4><<<nblk, BTH, 0, st>>>(a1g, xng, dpool, pmask, w2t, slab, xg_sync);
       break;
     default:
       break;   // bind.cpp validates bands

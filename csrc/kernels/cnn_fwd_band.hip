@@ -31,12 +31,14 @@ struct FwdBand {
   static constexpr int LUT = MS + RP * HP * C2;
   static constexpr int W = LUT + 512;               // fp32 w1 [288] | b1 [32] | b2 [64]
   static constexpr int SPARE = W + 1536;            // dropped conv1 stores (64 lanes x 8 B)
-  static constexpr int TOTAL = SPARE + 512;
+  static constexpr int W2 = SPARE + 512;            // conv2 B fragments (fragment-major W2)
+  static constexpr int TOTAL = W2 + 36 * 1024;
   static constexpr int NT1 = (AR * IMG + 15) / 16;  // conv1 tiles (16 virtual pixels)
   static constexpr int TPW1 = (NT1 + 7) / 8;
   static constexpr int NT2 = 3 * RP;                // conv2 tiles (4 pooled px x 2x2 window)
   static constexpr int TPW2 = (NT2 + 3) / 4;        // per wave pair
-  static_assert(TOTAL <= 65536 && A1 % 128 == 0 && PS % 16 == 0 && MS % 16 == 0, "fwd band LDS");
+  static_assert(TOTAL <= 81920 && A1 % 128 == 0 && PS % 16 == 0 && MS % 16 == 0 && W2 % 128 == 0,
+                "fwd band LDS (two workgroups per CU)");
 };
 
 template <int R, bool TRAIN>
@@ -45,7 +47,7 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
-    uint8_t* __restrict__ xg, int32_t* __restrict__ ylab) {
+    bf16* __restrict__ a1g, bf16* __restrict__ xng, int32_t* __restrict__ ylab) {
   using L = FwdBand<R>;
   constexpr int S = L::S;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
@@ -88,6 +90,18 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
     lab = labels[src + vz];
   }
+  // conv2's B fragments (fragment-major W2, 36 x 1 KB) by LDS-DMA on waves 2, 3, 6, 7, which
+  // load nothing else (vmcnt is per wave: the image and weight waves never wait for it);
+  // per-wave fragment loads were 18 load instructions in every wave
+  if ((wave & 3) >= 2) {
+    const int dw = (wave >> 2) * 2 + (wave & 1);  // 0..3
+    const unsigned wbase = lds_addr(smem) + L::W2;
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int blk = dw + 4 * m;
+      glds16(w2 + (blk * 64 + lane) * 8, wbase + blk * 1024);
+    }
+  }
   bf16* lut = reinterpret_cast<bf16*>(smem + L::LUT);
   if (tid >= 256) lut[tid - 256] = to_bf16(pdm_normalize(tid - 256));
   float* wl = reinterpret_cast<float*>(smem + L::W);
@@ -109,9 +123,11 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
                        lut[xw >> 24], lut[xn & 0xff], lut[(xn >> 8) & 0xff]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) x3[4 * tid + i] = bf16x4{v[i], v[i + 1], v[i + 2], bf16{}};
-    // training: the band's own rows of the gathered image (the last band also rows 24-27)
+    // training: the band's own rows of the normalised bf16 image (the last band also rows
+    // 24-27) for the backward's conv1 weight gradient
     const int own = band == S - 1 ? XW : R * 7;
-    if (TRAIN && tid < own) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[d0 * 7 + tid] = xw;
+    if (TRAIN && tid < own)
+      reinterpret_cast<bf16x4*>(xng + (int64_t)img * 784)[d0 * 7 + tid] = bf16x4{v[0], v[1], v[2], v[3]};
   }
   __syncthreads();
   PDM_STAMP(2);
@@ -120,13 +136,6 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
   float b2r[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) b2r[j] = wl[320 + nh * 32 + j * 16 + i16];
-  bf16x8 wb[9][2];
-  auto load_wb = [&](int f) __attribute__((always_inline)) {   // fragments 3f .. 3f + 2
-#pragma unroll
-    for (int e = 3 * f; e < 3 * f + 3; ++e)
-      wb[e >> 1][e & 1] = *reinterpret_cast<const bf16x8*>(
-          w2 + ((int64_t)((nh * 2 + (e & 1)) * 9 + (e >> 1)) * 64 + lane) * 8);
-  };
   bf16x4 w1f[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -143,18 +152,8 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
       vv[k] = (wave + 8 * k) * 16 + i16;
       bx[k] = x3[min(vv[k], L::AR * IMG - 1) + rowg];
     }
-    // the 18 conv2 B fragments are issued behind the image (as cnn_fwd), spread over the
-    // conv1 tiles (6 batches of 3)
 #pragma unroll
     for (int k = 0; k < L::TPW1; ++k) {
-      if (k < 6) {
-        if (k + 1 == L::TPW1) {
-#pragma unroll
-          for (int f = k; f < 6; ++f) load_wb(f);
-        } else {
-          load_wb(k);
-        }
-      }
       const int y = vv[k] / IMG, x = vv[k] - y * IMG;
       const bool ok = y < L::AR && x < H1;
       const int ab = (vv[k] - 2 * y) * 64 + a1c;
@@ -168,8 +167,18 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
       }
     }
   }
+  if ((wave & 3) >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W2 DMA landed
   __syncthreads();
   PDM_STAMP(3);
+  if (TRAIN) {
+    // the band's own a1 rows (the last band also 24, 25), in the LDS image's swizzled layout,
+    // for the backward (cnn_bwd_band copies them back by LDS-DMA instead of recomputing
+    // conv1); a contiguous byte range of the image's [26][26][32] a1
+    const int arows = band == S - 1 ? R + 2 : R;
+    const uint4* srcv = reinterpret_cast<const uint4*>(a1s);
+    uint4* dstv = reinterpret_cast<uint4*>(a1g + (int64_t)img * (P1 * C1) + d0 * H1 * C1);
+    for (int i = tid; i < arows * H1 * 4; i += FTH) dstv[i] = srcv[i];
+  }
 
   // 3. conv2 implicit GEMM over the band's tiles (local pooled row pyl, px0 % 4 == 0)
   const int q = i16 >> 2, s = i16 & 3;
@@ -187,9 +196,14 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     if (tt >= L::NT2) break;
     const int pyl = tt / 3, px0 = 4 * (tt - pyl * 3);
     const char* tb = a1s + (2 * pyl * H1 + 2 * px0) * 64;
-    bf16x8 a[9];
+    bf16x8 a[9], wb[9][2];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) a[t] = *reinterpret_cast<const bf16x8*>(tb + aoff[t]);
+    for (int t = 0; t < 9; ++t) {
+      a[t] = *reinterpret_cast<const bf16x8*>(tb + aoff[t]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        wb[t][j] = *reinterpret_cast<const bf16x8*>(smem + L::W2 + (((nh * 2 + j) * 9 + t) * 64 + lane) * 16);
+    }
     f32x4 acc[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[j] = f32x4{b2r[j], b2r[j], b2r[j], b2r[j]};
@@ -228,15 +242,15 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
 template <int R>
 void launch_band(const uint8_t* images, const int32_t* labels, const int32_t* idx, int64_t nrow,
                  const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
-                 const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
-                 int32_t* ylab, hipStream_t st) {
+                 const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, __bf16* a1g,
+                 __bf16* xng, int32_t* ylab, hipStream_t st) {
   const int nblk = B * FwdBand<R>::S;
-  if (xg != nullptr)
+  if (a1g != nullptr)
     cnn_fwd_band_kernel<R, true><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1,
-                                                       w2, b2, pool, pmask, xg, ylab);
+                                                       w2, b2, pool, pmask, a1g, xng, ylab);
   else
     cnn_fwd_band_kernel<R, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1,
-                                                        b1, w2, b2, pool, pmask, xg, ylab);
+                                                        b1, w2, b2, pool, pmask, a1g, xng, ylab);
 }
 
 }  // namespace
@@ -244,18 +258,19 @@ void launch_band(const uint8_t* images, const int32_t* labels, const int32_t* id
 void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                          int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
-                         __bf16* pool, uint8_t* pmask, uint8_t* xg, int32_t* ylab, hipStream_t st) {
+                         __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, int32_t* ylab,
+                         hipStream_t st) {
   switch (bands) {
     case 2:
-      launch_band<12>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, xg,
+      launch_band<12>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
                       ylab, st);
       break;
     case 3:
-      launch_band<8>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, xg,
+      launch_band<8>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
                      ylab, st);
       break;
     case 6:
-      launch_band<4>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, xg,
+      launch_band<4>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
                      ylab, st);
       break;
     default:

@@ -41,6 +41,18 @@ def frag_major(w: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1, 4).contiguous().reshape(-1)   # [mb][kb][g][i][j]
 
 
+def a1_swizzled(a1: torch.Tensor) -> torch.Tensor:
+    """[B, 26*26, 32] conv1 activations -> the swizzled a1 image cnn_fwd_band writes and
+    cnn_bwd_band reads (cnn_common.h a1_off: the 16-B chunk c // 8 of pixel (y, x) stored at
+    chunk (c // 8) ^ (x & 3)).  Flat 1-D result."""
+    b = a1.shape[0]
+    t = a1.reshape(b, 26, 26, 4, 8)
+    x = torch.arange(26).view(1, 1, 26, 1)
+    src = torch.arange(4).view(1, 1, 1, 4) ^ (x & 3)           # stored chunk j holds chunk j ^ (x & 3)
+    out = torch.gather(t, 3, src.expand(b, 26, 26, 4).unsqueeze(-1).expand(b, 26, 26, 4, 8))
+    return out.reshape(-1).contiguous()
+
+
 def frag_major_t(w: torch.Tensor) -> torch.Tensor:
     """The transpose of [rows][cols] in the fragment-major layout (kernels.h shadow_t_pos)."""
     return frag_major(w.t())
@@ -108,6 +120,12 @@ class CnnStep(GpuStepBase):
                                      device=dev)
         self.dpool = torch.empty(B * 9216, dtype=bf16, device=dev)
         self.ipb = choose_ipb(B)
+        # row-band steps (small batches): the forward hands a1 and the normalised x to the
+        # backward (cnn_fwd_band -> cnn_bwd_band) instead of the backward recomputing conv1
+        nband = max(b for b in range(1, B + 1) if choose_bands(b) > 1) if \
+            any(choose_bands(b) > 1 for b in range(1, B + 1)) else 0
+        self.a1g = torch.empty(max(nband, 1) * 676 * 32, dtype=bf16, device=dev)
+        self.xng = torch.empty(max(nband, 1) * 784, dtype=bf16, device=dev)
         # slabs for every batch size this step runs (the ragged tail may split into more
         # bands than the full batch)
         self.conv_nblk = max(conv_blocks(C, b) for b in range(1, B + 1))
@@ -135,6 +153,12 @@ class CnnStep(GpuStepBase):
         self.fuse_fc1 = (self.fuse_conv_reduce and self.opt.kind == "sgd" and
                          os.environ.get("PDM_FUSE_FC1", "1") != "0")
         self._fused = {}
+        # RCCL data plane: defer the fc-bucket update past the next step's cnn_fwd so the
+        # 4.7 MB all-reduce overlaps it (True), or reduce both buckets in one grouped RCCL
+        # launch and update every parameter in one optimizer launch (False: fewer launches
+        # when the transfer is short).  bench.py calibrates both; PDM_FC_CARRY=0/1 forces.
+        env = os.environ.get("PDM_FC_CARRY")
+        self.fc_carry = True if env is None else env != "0"
         self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
         self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
         self.refresh_shadows()
@@ -226,7 +250,8 @@ class CnnStep(GpuStepBase):
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
-        carry = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
+        carry = (self.reducer.active and getattr(self.reducer, "kind", None) == "rccl" and
+                 self.fc_carry)
         streamed = self.reducer.streamed
         if streamed:
             self.reducer.begin(n)        # one persistent xgmi collective for the n steps
@@ -250,7 +275,7 @@ class CnnStep(GpuStepBase):
         bands = choose_bands(B)
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                  self.pmask, self.xg, self.ylab, bands)
+                  self.pmask, self.xg, self.ylab, bands, self.a1g, self.xng)
         if carry_in:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(self._bucket_segments()[0])
@@ -273,7 +298,7 @@ class CnnStep(GpuStepBase):
         # streamed xgmi: cnn_bwd's first workgroup publishes the fc bucket to the
         # persistent collective, which then reduces it beside cnn_bwd
         C.cnn_bwd(self.xg, P["conv1.weight"], P["conv1.bias"], self.dpool, self.pmask, self.w2t, B,
-                  ipb, self.conv_slab, xs, bands)
+                  ipb, self.conv_slab, xs, bands, self.a1g, self.xng)
         if self.fuse_conv_reduce:
             # world_size 1: no all-reduce, the conv slab reduction runs inside the update
             self.launch_optimizer(self._fused_segments(nblk))
@@ -308,6 +333,12 @@ class CnnStep(GpuStepBase):
         # for cnn_bwd or push part of it into a second round.  The small conv bucket goes
         # first (the next forward needs it); the 4.7 MB fc bucket keeps reducing while the
         # conv update and the next step's cnn_fwd run.
+        if not self.fc_carry:
+            # one grouped RCCL launch for both buckets, one optimizer launch for everything
+            self.reducer.all_ready()
+            self.reducer.finalize()
+            self.launch_optimizer()
+            return
         b0, b1 = self._bucket_segments()
         self.reducer.bucket_ready(1)
         self.reducer.bucket_ready(0)

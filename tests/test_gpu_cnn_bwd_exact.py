@@ -5,7 +5,7 @@ fed to the reference exactly, so only fp32-vs-fp64 summation order differs."""
 import pytest
 import torch
 
-from pytorch_distributed_mnist_amd.runtime.cnn_step import frag_major, frag_major_t
+from pytorch_distributed_mnist_amd.runtime.cnn_step import a1_swizzled, frag_major, frag_major_t
 
 pytestmark = pytest.mark.gpu
 
@@ -43,8 +43,11 @@ def test_cnn_bwd_exact(gpu, B, ipb, bands):
     nblk = C.cnn_bwd_nblk(B, ipb, bands)
     assert nblk == (B * bands if bands > 1 else -(-B // ipb))
     slab = torch.full((nblk * C.CNN_CONV_SLAB,), float("nan"), device=gpu)   # every entry written
+    # the band backward reads the forward's a1 image (swizzled) and normalised bf16 x
+    a1g = a1_swizzled(a1).to(gpu)
+    xng = xn.to(torch.bfloat16).reshape(-1).to(gpu)
     C.cnn_bwd(xg.to(gpu), w1.to(gpu), b1.to(gpu), dpool.to(gpu), pmask.to(gpu), w2t.to(gpu), B,
-              ipb, slab, None, bands)
+              ipb, slab, None, bands, a1g, xng)
     gw2 = torch.zeros(64 * 288, device=gpu)
     gb2 = torch.zeros(64, device=gpu)
     gw1 = torch.zeros(288, device=gpu)

@@ -74,7 +74,8 @@ def test_grad_reducer_grouped_all_ready(gpu):
     comm.close()
 
 
-def test_cnn_step_through_rccl_reducer_matches_local(gpu):
+@pytest.mark.parametrize("carry", [True, False])
+def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry):
     """The world_size > 1 step structure (unfused conv reduction, grouped RCCL all-reduce of
     both buckets, finalize) with a forced 1-rank RCCL communicator, graph-captured, gives
     the same parameters as the world_size-1 fast path."""
@@ -90,6 +91,7 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu):
                                 momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=force,
                                 transport="rccl")
         assert p.gpu.fuse_conv_reduce == (not force)
+        p.gpu.fc_carry = carry
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         p.train_epoch()

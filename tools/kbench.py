@@ -55,7 +55,7 @@ def main():
       ks = {
           "cnn_fwd": lambda: C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, z, B, B,
                                        P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"],
-                                       st.pool, st.pmask, st.xg, st.ylab),
+                                       st.pool, st.pmask, st.xg, st.ylab, bands, st.a1g, st.xng),
           "fc1_fwd": lambda: C.fc1_fwd(st.pool, st.wf1, st.part, B, S),
           "cnn_head": lambda: C.cnn_head(st.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                                          st.ylab, True, st.dh, st.dht, ldt, st.head_slab,
@@ -65,7 +65,7 @@ def main():
                                        G["fc1.bias"], st.metrics.train_view(),
                                        st._fc_update() if st.fuse_fc1 else None),
           "cnn_bwd": lambda: C.cnn_bwd(st.xg, P["conv1.weight"], P["conv1.bias"], st.dpool, st.pmask,
-                                       st.w2t, B, ipb, st.conv_slab, None, bands),
+                                       st.w2t, B, ipb, st.conv_slab, None, bands, st.a1g, st.xng),
           "conv_reduce": lambda: C.conv_reduce(st.conv_slab, nblk, G["conv2.weight"],
                                                G["conv2.bias"], G["conv1.weight"], G["conv1.bias"]),
           # the training step's update: the slab-fused launch at world size 1

@@ -26,7 +26,7 @@ torch.cuda.synchronize()
 C = p.gpu.C
 PH = {"fwd_band": ["start", "weights+image(barrier)", "x3(barrier)", "conv1(barrier)",
                    "conv2(barrier)", "end"],
-      "bwd_band": ["start", "loads issued", "LUT(barrier)", "conv1 done", "scatter done",
+      "bwd_band": ["start", "loads issued", "zero fills", "-", "scatter done",
                    "staged(barrier)", "wgrad done w0", "dgrad done w4", "compute(barrier)", "end"]}
 for which, names in PH.items():
     st = C.read_stamps(which).double()
