@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--batch-per-rank", type=int, default=NODE_BATCH,
                     help="per-rank batch of the weak-scaling measurement")
     ap.add_argument("--scaling", choices=["weak", "strong", "both"], default="both")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default=None,
+                    help="CNN compute dtype (default bf16; fp32 = the reference's precision on the "
+                         "fp32 MFMA); the Linear model always runs fp32")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default=None)
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--no-graphs", dest="graphs", action="store_false")
@@ -94,7 +97,7 @@ def main():
     spec = get_spec(model)
     parallel.verify_params_across_ranks(spec, rank, ws)
     comm = parallel.make_comm(ctx, force_native=force_comm)
-    dtype = "bf16" if model == "cnn" else "fp32"
+    dtype = (a.dtype or "bf16") if model == "cnn" else "fp32"
     optname = a.optimizer or ("sgd" if model == "cnn" else "adam")
     lr = a.lr if a.lr is not None else (0.01 if optname == "sgd" else 1e-3)
 

@@ -432,7 +432,7 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
               at::Tensor bf2, at::Tensor ylab, bool train, c10::optional<at::Tensor> dh,
               c10::optional<at::Tensor> dht, int64_t ldt, c10::optional<at::Tensor> slab,
               at::Tensor metrics, c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1,
-              c10::optional<at::Tensor> xg) {
+              c10::optional<at::Tensor> xg, c10::optional<at::Tensor> dh32) {
   c10::DeviceGuard g(part.device());
   TORCH_CHECK(B >= 1, "B must be >= 1");
   need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
@@ -446,21 +446,29 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
   need_numel(metrics, 3, "metrics");
   __bf16 *pdh = nullptr, *pdht = nullptr;
   float* pslab = nullptr;
+  float* pdh32 = nullptr;
   if (train) {
     TORCH_CHECK(ldt % 32 == 0 && ldt >= B, "ldt must be a multiple of 32 and >= B");
-    TORCH_CHECK(dh && dht && slab, "train mode needs dh, dht, slab");
-    need_min(*dh, at::kBFloat16, ldt * CNN_HID, "dh");
-    need_min(*dht, at::kBFloat16, ldt * CNN_HID, "dht");
+    TORCH_CHECK(slab, "train mode needs slab");
+    if (dh32.has_value() && dh32->defined()) {     // fp32 step: dh in fp32, row-major
+      need_min(*dh32, at::kFloat, ldt * CNN_HID, "dh32");
+      need_aligned(dh32->data_ptr(), 8, "dh32");
+      pdh32 = dh32->data_ptr<float>();
+    } else {
+      TORCH_CHECK(dh && dht, "train mode needs dh and dht (or dh32)");
+      need_min(*dh, at::kBFloat16, ldt * CNN_HID, "dh");
+      need_min(*dht, at::kBFloat16, ldt * CNN_HID, "dht");
+      pdh = ptr<__bf16>(*dh);
+      pdht = ptr<__bf16>(*dht);
+    }
     need_min(*slab, at::kFloat, (int64_t)cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)) * CNN_HEAD_SLAB,
              "head slab");
-    pdh = ptr<__bf16>(*dh);
-    pdht = ptr<__bf16>(*dht);
     pslab = slab->data_ptr<float>();
   }
   launch_cnn_head(part.data_ptr<float>(), (int)splitk, (int)B, bf1.data_ptr<float>(),
                   wf2.data_ptr<float>(), bf2.data_ptr<float>(), ylab.data_ptr<int32_t>(), train, pdh,
                   pdht, (int)ldt, pslab, metrics.data_ptr<double>(), opt_i64(c0), opt_i64(c1),
-                  train ? xg_step(xg) : nullptr, cur_stream(part));
+                  train ? xg_step(xg) : nullptr, pdh32, cur_stream(part));
 }
 
 // fc_update (world size 1, optional): (kind, p, g, m, v or None, shadow, lr, step, beta1,
@@ -591,6 +599,101 @@ void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, 
 
 int64_t cnn_bwd_nblk(int64_t B, int64_t ipb, int64_t bands) { return conv_blocks(B, ipb, bands); }
 
+// ------------------------------------------------------------------ CNN fp32 (cnn_f32.hip)
+void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr, int64_t bfull,
+             int64_t B, at::Tensor w1, at::Tensor b1, at::Tensor w2, at::Tensor b2,
+             at::Tensor pool, c10::optional<at::Tensor> pmask, c10::optional<at::Tensor> a1g,
+             c10::optional<at::Tensor> xng, at::Tensor ylab) {
+  c10::DeviceGuard g(images.device());
+  need(images, at::kByte, "images");
+  need(labels, at::kInt, "labels");
+  TORCH_CHECK(images.dim() == 2 && images.size(1) == 784 && images.size(0) >= 1, "images [N, 784]");
+  TORCH_CHECK(labels.numel() == images.size(0), "labels [N]");
+  need_aligned(images.data_ptr(), 4, "images");
+  TORCH_CHECK(B >= 1 && (!ctr.has_value() ? images.size(0) >= B : B <= bfull), "batch size");
+  if (ctr.has_value()) need(*ctr, at::kLong, "ctr");
+  need(w1, at::kFloat, "w1");
+  need(b1, at::kFloat, "b1");
+  need(w2, at::kFloat, "w2");
+  need(b2, at::kFloat, "b2");
+  TORCH_CHECK(w1.numel() == 288 && b1.numel() == 32 && w2.numel() == 64 * 288 && b2.numel() == 64,
+              "conv weights");
+  for (const void* q : {w1.data_ptr(), b1.data_ptr(), b2.data_ptr()}) need_aligned(q, 16, "conv weight");
+  need_min(pool, at::kFloat, B * CNN_FEAT, "pool");
+  need(ylab, at::kInt, "ylab");
+  need_min(ylab, at::kInt, B, "ylab");
+  const bool train = a1g.has_value() && a1g->defined();
+  if (train) {
+    TORCH_CHECK(pmask.has_value() && xng.has_value(), "training needs pmask, a1g and xng");
+    need_min(*pmask, at::kByte, B * CNN_FEAT, "pmask");
+    need_min(*a1g, at::kFloat, B * 676 * 32, "a1g");
+    need_min(*xng, at::kFloat, B * 784, "xng");
+    need_aligned(a1g->data_ptr(), 16, "a1g");
+    need_aligned(xng->data_ptr(), 16, "xng");
+  }
+  launch_f32_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), images.size(0),
+                 ctr.has_value() ? ctr->data_ptr<int64_t>() : nullptr, (int)bfull, (int)B,
+                 w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+                 pool.data_ptr<float>(), train ? pmask->data_ptr<uint8_t>() : nullptr,
+                 train ? a1g->data_ptr<float>() : nullptr, train ? xng->data_ptr<float>() : nullptr,
+                 ylab.data_ptr<int32_t>(), cur_stream(images));
+}
+
+void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int64_t splitk) {
+  c10::DeviceGuard g(pool.device());
+  TORCH_CHECK(B >= 1 && splitk >= 1 && 288 % splitk == 0, "splitk must divide 288");
+  need_min(pool, at::kFloat, B * CNN_FEAT, "pool");
+  need(w1, at::kFloat, "w1");
+  TORCH_CHECK(w1.numel() == (int64_t)CNN_HID * CNN_FEAT, "fc1 weight");
+  need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
+  for (const void* q : {pool.data_ptr(), w1.data_ptr()}) need_aligned(q, 16, "fc1 operand");
+  launch_f32_fc1_fwd(pool.data_ptr<float>(), w1.data_ptr<float>(), part.data_ptr<float>(), (int)B,
+                     (int)splitk, cur_stream(pool));
+}
+
+void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int64_t B,
+                 at::Tensor gwf1, at::Tensor dpool, at::Tensor head_slab, at::Tensor gwf2,
+                 at::Tensor gbf2, at::Tensor gbf1, at::Tensor metrics) {
+  c10::DeviceGuard g(dh.device());
+  TORCH_CHECK(B >= 1 && ldt % 32 == 0 && ldt >= B, "ldt must be a multiple of 32 and >= B");
+  need_min(dh, at::kFloat, ldt * CNN_HID, "dh32");
+  need_min(pool, at::kFloat, B * CNN_FEAT, "pool");
+  need(w1, at::kFloat, "w1");
+  TORCH_CHECK(w1.numel() == (int64_t)CNN_HID * CNN_FEAT, "fc1 weight");
+  need(gwf1, at::kFloat, "gwf1");
+  TORCH_CHECK(gwf1.numel() == (int64_t)CNN_HID * CNN_FEAT, "fc1 grad");
+  need_min(dpool, at::kFloat, B * CNN_FEAT, "dpool");
+  const int hb = cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS));
+  need_min(head_slab, at::kFloat, (int64_t)hb * CNN_HEAD_SLAB, "head slab");
+  need(gwf2, at::kFloat, "gwf2");
+  need(gbf2, at::kFloat, "gbf2");
+  need(gbf1, at::kFloat, "gbf1");
+  TORCH_CHECK(gwf2.numel() == 1280 && gbf2.numel() == 10 && gbf1.numel() == 128, "head grads");
+  need(metrics, at::kDouble, "metrics");
+  need_numel(metrics, 3, "metrics");
+  for (const void* q : {dh.data_ptr(), pool.data_ptr(), w1.data_ptr()}) need_aligned(q, 16, "fc1 operand");
+  launch_f32_fc1_bwd(dh.data_ptr<float>(), (int)ldt, pool.data_ptr<float>(), w1.data_ptr<float>(),
+                     (int)B, gwf1.data_ptr<float>(), dpool.data_ptr<float>(),
+                     head_slab.data_ptr<float>(), hb, gwf2.data_ptr<float>(), gbf2.data_ptr<float>(),
+                     gbf1.data_ptr<float>(), metrics.data_ptr<double>(), cur_stream(dh));
+}
+
+void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor pmask, at::Tensor w2,
+                  int64_t B, at::Tensor slab) {
+  c10::DeviceGuard g(a1g.device());
+  TORCH_CHECK(B >= 1, "B must be >= 1");
+  need_min(a1g, at::kFloat, B * 676 * 32, "a1g");
+  need_min(xng, at::kFloat, B * 784, "xng");
+  need_min(dpool, at::kFloat, B * CNN_FEAT, "dpool");
+  need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
+  need(w2, at::kFloat, "w2");
+  TORCH_CHECK(w2.numel() == 64 * 288, "conv2 weight");
+  need_min(slab, at::kFloat, (int64_t)f32_conv_bwd_blocks((int)B) * CNN_CONV_SLAB, "conv slab");
+  launch_f32_conv_bwd(a1g.data_ptr<float>(), xng.data_ptr<float>(), dpool.data_ptr<float>(),
+                      pmask.data_ptr<uint8_t>(), w2.data_ptr<float>(), (int)B, slab.data_ptr<float>(),
+                      cur_stream(a1g));
+}
+
 // Upload an instantiated hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device
 // on the current stream, so its first replay inside a timed region costs the same as later ones.
 void graph_upload(int64_t exec, int64_t device) {
@@ -653,7 +756,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
         py::arg("dht"), py::arg("ldt"), py::arg("slab"), py::arg("metrics"), py::arg("c0"),
-        py::arg("c1"), py::arg("xg") = py::none());
+        py::arg("c1"), py::arg("xg") = py::none(), py::arg("dh32") = py::none());
   m.def("fc1_bwd", &fc1_bwd, py::arg("dh"), py::arg("dht"), py::arg("ldt"), py::arg("pool"),
         py::arg("wf1t"), py::arg("B"), py::arg("gwf1"), py::arg("dpool"), py::arg("head_slab"),
         py::arg("gwf2"), py::arg("gbf2"), py::arg("gbf1"), py::arg("metrics"),
@@ -663,6 +766,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("xg_sync") = py::none(), py::arg("bands") = 1, py::arg("a1g") = py::none(),
         py::arg("xng") = py::none());
   m.def("conv_reduce", &conv_reduce);
+  m.def("f32_fwd", &f32_fwd, py::arg("images"), py::arg("labels"), py::arg("ctr"), py::arg("bfull"),
+        py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"), py::arg("pool"),
+        py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"));
+  m.def("f32_fc1_fwd", &f32_fc1_fwd);
+  m.def("f32_fc1_bwd", &f32_fc1_bwd);
+  m.def("f32_conv_bwd", &f32_conv_bwd);
+  m.def("f32_conv_bwd_nblk", [](int64_t B) { return (int64_t)f32_conv_bwd_blocks((int)B); });
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);
   m.def("read_stamps", &read_stamps);
   m.def("graph_upload", &graph_upload);

@@ -170,7 +170,7 @@ void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, i
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
-                     unsigned* c2, hipStream_t st);
+                     unsigned* c2, float* dh32, hipStream_t st);
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
@@ -188,6 +188,24 @@ void launch_cnn_bwd_band(const __bf16* a1g, const __bf16* xng, const __bf16* dpo
                          unsigned* xg_sync, hipStream_t st);
 void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, float* gw1, float* gb1,
                         hipStream_t st);
+
+// ---------------------------------------------------------------- CNN (fp32, cnn_f32.hip)
+// The reference's precision on the fp32 MFMA (v_mfma_f32_16x16x4_f32).  fp32 layouts as the
+// bf16 path (pool [B][12*12][64], pmask, conv2 weight [co][tap][ci], fc1 weight [128][9216]);
+// a1g [B][676][32] and xng [B][784] carry the forward's conv1 activations and normalised
+// image to the backward; dh32 [ldt][128] is cnn_head's fp32 dh (launch_cnn_head dh32 != null).
+void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
+                    int bfull, int B, const float* w1, const float* b1, const float* w2,
+                    const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
+                    int32_t* ylab, hipStream_t st);
+void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,
+                        hipStream_t st);
+void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
+                        float* gwf1, float* dpool, const float* head_slab, int head_blocks,
+                        float* gwf2, float* gbf2, float* gbf1, double* metrics, hipStream_t st);
+int f32_conv_bwd_blocks(int B);
+void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
+                         const uint8_t* pmask, const float* w2, int B, float* slab, hipStream_t st);
 
 // diagnostic timestamps (all zero unless built with PDM_STAMPS=1)
 void read_stamps_fwd(unsigned long long* host);

@@ -1,0 +1,551 @@
+// fp32 CNN step on gfx950: the reference's precision (multi_proc_single_gpu.py trains in fp32,
+// S:185-191) on the fp32 matrix cores, v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32
+// accumulation).  The same chain and fusions as the bf16 kernels, without the bf16 operand
+// copies (the MFMAs read the fp32 master weights directly):
+//
+//   f32_fwd      one image / workgroup: normalise -> conv1 + ReLU (VALU, exact fp32) into an
+//                LDS a1 image -> conv2 implicit GEMM (M = 576 pixels ordered (pooled pixel,
+//                window position), N = 64, K = 288) with bias + ReLU + 2x2 max-pool fused in
+//                the epilogue -> pooled activations + pool mask; training also writes a1 and
+//                the normalised x for the backward
+//   f32_fc1_fwd  split-K GEMM pool . W1^T -> fp32 partials (the cnn_head kernel sums them,
+//                applies bias + ReLU, fc2, CE and the head backward, writing dh in fp32)
+//   f32_fc1_bwd  dW1 tiles (K = batch) | dX tiles (K = 128) | head-slab reduction
+//   f32_conv_bwd image row band / workgroup: dz2 = maxpool^-1(dpool) -> conv2 dgrad fused with
+//                relu'(a1) and the conv1 weight/bias gradient, conv2 wgrad -> one fp32 slab per
+//                workgroup (the bf16 kernels' slab layout: conv_reduce / the fused optimizer)
+//
+// MFMA 16x16x4 f32 operand layout, lane l = 16 g + i: A[m = i][k = g], B[k = g][n = i],
+// D[m = 4 g + r][n = i] for r = 0..3.
+#include "cnn_common.h"
+
+namespace {
+
+using namespace cnn;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------ f32_fwd
+constexpr int FT = 512;
+constexpr int A1S = 33;                           // a1 pixel stride in floats (bank spread)
+constexpr int FX_XS = 0;                          // fp32 x [784]
+constexpr int FX_WS = 3136;                       // fp32 w1 [288] | b1 [32] | b2 [64]
+constexpr int FX_A1 = FX_WS + 1536;               // fp32 a1 [676][33]
+constexpr int FX_W2 = FX_A1 + P1 * A1S * 4;       // fp32 W2 half [288 k][32 co], swizzled
+constexpr int FX_TOTAL = FX_W2 + 288 * 32 * 4;
+static_assert(FX_TOTAL <= 163840 && FX_A1 % 16 == 0 && FX_W2 % 16 == 0, "f32_fwd LDS");
+
+// W2 half: element (k, c) at k * 32 + (c ^ ((k & 2) << 3)) -- the B reads of a k-step (4
+// consecutive k, 16 consecutive c) hit 64 distinct banks
+__device__ __forceinline__ int w2h_off(int k, int c) { return k * 32 + (c ^ ((k & 2) << 3)); }
+
+template <bool TRAIN>
+__global__ __launch_bounds__(FT, 1) void f32_fwd_kernel(
+    const uint8_t* __restrict__ images, const int32_t* __restrict__ labels, int64_t nrow,
+    const int64_t* __restrict__ ctr, int bfull, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ pool, uint8_t* __restrict__ pmask, float* __restrict__ a1g,
+    float* __restrict__ xng, int32_t* __restrict__ ylab) {
+  __shared__ __attribute__((aligned(16))) char smem[FX_TOTAL];
+  float* xs = reinterpret_cast<float*>(smem + FX_XS);
+  float* ws = reinterpret_cast<float*>(smem + FX_WS);
+  float* a1 = reinterpret_cast<float*>(smem + FX_A1);
+  float* w2h = reinterpret_cast<float*>(smem + FX_W2);
+  const int img = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  // 0. small weights -> LDS, the image (epoch-buffer row ctr * bfull + img, or row img)
+  const int wt = tid - 256;
+  if (wt >= 0 && wt < 96) {
+    const float4 q = wt < 72 ? reinterpret_cast<const float4*>(w1)[wt]
+                     : wt < 80 ? reinterpret_cast<const float4*>(b1)[wt - 72]
+                               : reinterpret_cast<const float4*>(b2)[wt - 80];
+    reinterpret_cast<float4*>(ws)[wt] = q;
+  }
+  const int64_t row = min(ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img, nrow - 1);
+  if (tid < 196) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(images + row * 784)[tid];
+    const float4 x = make_float4(pdm_normalize(v & 0xff), pdm_normalize((v >> 8) & 0xff),
+                                 pdm_normalize((v >> 16) & 0xff), pdm_normalize(v >> 24));
+    reinterpret_cast<float4*>(xs)[tid] = x;
+    if (TRAIN) reinterpret_cast<float4*>(xng + (int64_t)img * 784)[tid] = x;
+  }
+  if (tid == 64) ylab[img] = labels[row];
+  __syncthreads();
+  // 1. conv1 + bias + ReLU: thread = pixel, all 32 channels (weights are LDS broadcasts)
+  for (int p = tid; p < P1; p += FT) {
+    const int y = p / H1, x = p - y * H1;
+    float xv[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) xv[t] = xs[(y + t / 3) * IMG + x + t % 3];
+#pragma unroll 2
+    for (int c4 = 0; c4 < C1 / 4; ++c4) {
+      float o[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int co = 4 * c4 + u;
+        float acc = ws[288 + co];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc = fmaf(ws[co * 9 + t], xv[t], acc);
+        o[u] = fmaxf(acc, 0.f);
+        a1[p * A1S + co] = o[u];
+      }
+      if (TRAIN)
+        reinterpret_cast<float4*>(a1g + ((int64_t)img * P1 + p) * C1)[c4] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  // 2. conv2 + bias + ReLU + max-pool, co in two halves (W2 half staged in LDS).  Tile tt =
+  // (pooled row py, pooled columns px0 .. px0 + 3): row i16 = 4 q + s is pooled pixel px0 + q,
+  // window position s = 2 dy + dx, so a lane's 4 accumulators (rows 4 g + r) are one window.
+  const int q = i16 >> 2, s = i16 & 3;
+  for (int nh = 0; nh < 2; ++nh) {
+    __syncthreads();   // a1 complete (nh = 0) / the previous half's B reads are done
+    for (int e = tid; e < 32 * 288; e += FT) {
+      const int c = e / 288, k = e - c * 288;
+      w2h[w2h_off(k, c)] = w2[(nh * 32 + c) * 288 + k];
+    }
+    __syncthreads();
+    float bias[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bias[nt] = ws[320 + nh * 32 + nt * 16 + i16];
+    for (int tt = wave; tt < 36; tt += 8) {
+      const int py = tt / 3, px0 = 4 * (tt - py * 3);
+      const int pb = (2 * py + (s >> 1)) * H1 + 2 * (px0 + q) + (s & 1);   // a1 pixel, tap 0
+      f32x4 acc[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[nt] = f32x4{bias[nt], bias[nt], bias[nt], bias[nt]};
+#pragma unroll 1
+      for (int tap = 0; tap < 9; ++tap) {
+        const float* ap = a1 + (pb + (tap / 3) * H1 + tap % 3) * A1S + g;
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) {
+          const int k = tap * 32 + c8 * 4 + g;
+          const float av = ap[c8 * 4];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[nt] = mfma4(av, w2h[w2h_off(k, nt * 16 + i16)], acc[nt]);
+        }
+      }
+      const int pp = py * HP + px0 + g;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int co = nh * 32 + nt * 16 + i16;
+        float m = acc[nt][0];
+        uint32_t oh = 1u;
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          const bool gt = acc[nt][r] > m;   // first position holding the max
+          m = gt ? acc[nt][r] : m;
+          oh = gt ? (1u << r) : oh;
+        }
+        const bool pos = m > 0.f;
+        pool[(int64_t)img * FEAT + pp * C2 + co] = pos ? m : 0.f;
+        if (TRAIN) pmask[(int64_t)img * FEAT + pp * C2 + co] = (uint8_t)(pos ? 0x80u | oh : 0u);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ f32_fc1_fwd
+// part[s][row][n] = sum_{k in split s} pool[row][k] W1[n][k]; workgroup = 32 rows x 128 n of
+// one split, 4 waves x 32 n; K in LDS-staged chunks of 32 (rows padded to 36 floats: the
+// A / B reads of a k-step hit 64 distinct banks)
+constexpr int KC = 32, KP = 36;
+
+__global__ __launch_bounds__(256) void f32_fc1_fwd_kernel(const float* __restrict__ pool,
+                                                          const float* __restrict__ w1,
+                                                          float* __restrict__ part, int B,
+                                                          int kchunk) {
+  __shared__ __attribute__((aligned(16))) float at[32 * KP];
+  __shared__ __attribute__((aligned(16))) float bt[HID * KP];
+  const int mtiles = (B + 31) / 32;
+  const int sidx = blockIdx.x / mtiles, mtile = blockIdx.x - sidx * mtiles;
+  const int b0 = mtile * 32, kbeg = sidx * kchunk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kbeg; k0 < kbeg + kchunk; k0 += KC) {
+    {
+      const int r = tid >> 3, c4 = tid & 7;    // A: 32 rows x 8 float4 (rows past B clamped)
+      const float4 v = *reinterpret_cast<const float4*>(pool + (int64_t)min(b0 + r, B - 1) * FEAT + k0 + 4 * c4);
+      *reinterpret_cast<float4*>(at + r * KP + 4 * c4) = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {              // B: 128 rows x 8 float4
+      const int e = tid + 256 * u, n = e >> 3, c4 = e & 7;
+      *reinterpret_cast<float4*>(bt + n * KP + 4 * c4) =
+          *reinterpret_cast<const float4*>(w1 + (int64_t)n * FEAT + k0 + 4 * c4);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KC / 4; ++kk) {
+      float a[2], b[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) a[mt] = at[(mt * 16 + i16) * KP + kk * 4 + g];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) b[nt] = bt[(wave * 32 + nt * 16 + i16) * KP + kk * 4 + g];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma4(a[mt], b[nt], acc[mt][nt]);
+    }
+    __syncthreads();
+  }
+  float* out = part + (int64_t)sidx * B * HID;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rowi = b0 + mt * 16 + 4 * g + r;
+      if (rowi < B) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) out[(int64_t)rowi * HID + wave * 32 + nt * 16 + i16] = acc[mt][nt][r];
+      }
+    }
+}
+
+// ------------------------------------------------------------------ f32_fc1_bwd
+constexpr int DWF = 64;                 // dW tile: 128 n x 64 features
+constexpr int DW_T = FEAT / DWF;        // 144
+constexpr int DXF = 256;                // dX tile: 32 rows x 256 features
+constexpr int DX_T = FEAT / DXF;        // 36 per 32 rows
+constexpr int HRB = (HEAD_SLAB + 63) / 64;   // head-slab reduction workgroups (23)
+constexpr int DHP = 144, PTP = 80, DXP = 132, WTP = 272;   // padded LDS row strides (floats)
+
+__global__ __launch_bounds__(256) void f32_fc1_bwd_kernel(
+    const float* __restrict__ dh, int ldt, const float* __restrict__ pool,
+    const float* __restrict__ w1, int B, float* __restrict__ gwf1, float* __restrict__ dpool,
+    const float* __restrict__ head_slab, int head_blocks, float* __restrict__ gwf2,
+    float* __restrict__ gbf2, float* __restrict__ gbf1, double* __restrict__ metrics) {
+  __shared__ __attribute__((aligned(16))) float sm[32 * DXP + 32 * WTP];   // 51.7 KB (dX role)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int nd = (ldt / 32) * DX_T;
+  const int bid = blockIdx.x;
+  if (bid < DW_T) {
+    // ---- dW1[n][k0 + f] = sum_b dh[b][n] pool[b][k0 + f]: M = n (wave: 32), N = 64 f, K = b
+    const int k0 = bid * DWF;
+    float* dhs = sm;                  // [32 b][DHP]
+    float* pts = sm + 32 * DHP;       // [32 b][PTP]
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < ldt; c0 += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {   // dh chunk: 32 rows x 32 float4 (rows >= B are zero)
+        const int e = tid + 256 * u, r = e >> 5, c4 = e & 31;
+        *reinterpret_cast<float4*>(dhs + r * DHP + 4 * c4) =
+            *reinterpret_cast<const float4*>(dh + (int64_t)(c0 + r) * HID + 4 * c4);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {   // pool chunk: 32 rows x 16 float4 (rows >= B -> 0)
+        const int e = tid + 256 * u, r = e >> 4, c4 = e & 15;
+        const float4 v = *reinterpret_cast<const float4*>(pool + (int64_t)min(c0 + r, B - 1) * FEAT + k0 + 4 * c4);
+        *reinterpret_cast<float4*>(pts + r * PTP + 4 * c4) = (c0 + r < B) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        float a[2], b[4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = dhs[(kk * 4 + g) * DHP + wave * 32 + mt * 16 + i16];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) b[nt] = pts[(kk * 4 + g) * PTP + nt * 16 + i16];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma4(a[mt], b[nt], acc[mt][nt]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wave * 32 + mt * 16 + 4 * g + r;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + nt * 16 + i16] = acc[mt][nt][r];
+      }
+    return;
+  }
+  if (bid < DW_T + nd) {
+    // ---- dpool[b][f] = sum_n dh[b][n] W1[n][f]: 32 rows x 256 f, K = 128 in 4 LDS chunks of
+    // 32 n; wave: 64 f (4 n-tiles) x 32 rows (2 m-tiles)
+    const int t = bid - DW_T;
+    const int b0 = (t / DX_T) * 32, f0 = (t - (t / DX_T) * DX_T) * DXF;
+    float* dhs = sm;                  // [32 rows][DXP]
+    float* wts = sm + 32 * DXP;       // [32 n][WTP]
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, r = e >> 5, c4 = e & 31;
+      *reinterpret_cast<float4*>(dhs + r * DXP + 4 * c4) =
+          *reinterpret_cast<const float4*>(dh + (int64_t)(b0 + r) * HID + 4 * c4);
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n0 = 0; n0 < HID; n0 += 32) {
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {   // W1 chunk: 32 n x 64 float4
+        const int e = tid + 256 * u, r = e >> 6, c4 = e & 63;
+        *reinterpret_cast<float4*>(wts + r * WTP + 4 * c4) =
+            *reinterpret_cast<const float4*>(w1 + (int64_t)(n0 + r) * FEAT + f0 + 4 * c4);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        float a[2], b[4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = dhs[(mt * 16 + i16) * DXP + n0 + kk * 4 + g];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) b[nt] = wts[(kk * 4 + g) * WTP + wave * 64 + nt * 16 + i16];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma4(a[mt], b[nt], acc[mt][nt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rowi = b0 + mt * 16 + 4 * g + r;
+        if (rowi < B) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            dpool[(int64_t)rowi * FEAT + f0 + wave * 64 + nt * 16 + i16] = acc[mt][nt][r];
+        }
+      }
+    return;
+  }
+  // ---- head-slab reduction: 64 slab columns x 4 groups per workgroup, fixed order
+  {
+    float* rs = sm;
+    double* rd = reinterpret_cast<double*>(sm + 256);
+    const int e = (bid - DW_T - nd) * 64 + (tid & 63), grp = tid >> 6;
+    const int ec = min(e, HEAD_SLAB - 1);
+    float sacc = 0.f;
+    double sd = 0.0;
+    for (int j0 = grp; j0 < head_blocks; j0 += 4 * 8) {   // 8 loads in flight, fixed order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = head_slab[(int64_t)min(j0 + 4 * u, head_blocks - 1) * HEAD_SLAB + ec];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float x = (j0 + 4 * u < head_blocks) ? v[u] : 0.f;
+        sacc += x;
+        sd += (double)x;
+      }
+    }
+    rs[tid] = sacc;
+    rd[tid] = sd;
+    __syncthreads();
+    if (tid < 64 && e < HEAD_SLAB) {
+      sacc = ((rs[tid] + rs[64 + tid]) + rs[128 + tid]) + rs[192 + tid];
+      sd = ((rd[tid] + rd[64 + tid]) + rd[128 + tid]) + rd[192 + tid];
+      if (e < NCLS * HID) gwf2[e] = sacc;
+      else if (e < NCLS * HID + NCLS) gbf2[e - NCLS * HID] = sacc;
+      else if (e < NCLS * HID + NCLS + HID) gbf1[e - NCLS * HID - NCLS] = sacc;
+      else if (e == HEAD_SLAB - 2) { metrics[0] += sd; metrics[2] += (double)B; }
+      else metrics[1] += sd;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ f32_conv_bwd
+// Workgroup = (image, row band of R = 4 conv2-output rows): 6 bands per image.  LDS (fp32):
+//   x    rows [d0, d0 + 8) of the normalised image                         1 KB
+//   a1   rows [d0, d0 + 6), 26 px, stride 33                               20.6 KB
+//   dz2  2 zero px + rows [d0 - 2, d0 + 7) x 26 px (cols 24, 25 zero: column -1 / -2 of a row
+//        wraps onto them), pixel stride 68 (conflict-free dgrad A reads)   64.2 KB
+//   W2^T [tap][co][ci], ci swizzled by (co & 2) << 3                      72 KB
+constexpr int CB_R = 4, CB_S = H2 / CB_R;
+constexpr int CB_XS = 0;
+constexpr int CB_A1 = 1024;
+constexpr int CB_DZ = CB_A1 + (CB_R + 2) * H1 * A1S * 4;
+constexpr int DZS = 68;
+constexpr int CB_ZR = CB_R + 5;
+constexpr int CB_W2 = (CB_DZ + (2 + CB_ZR * H1) * DZS * 4 + 15) / 16 * 16;
+constexpr int CB_TOTAL = CB_W2 + 9 * C2 * C1 * 4;
+static_assert(CB_TOTAL <= 163840, "f32_conv_bwd LDS");
+constexpr int SLB_DB2 = CNN_CONV_SLAB_DB2, SLB_DW1 = CNN_CONV_SLAB_DW1, SLB_DB1 = CNN_CONV_SLAB_DB1;
+
+__device__ __forceinline__ int w2t_off(int tap, int co, int ci) {
+  return (tap * C2 + co) * C1 + (ci ^ ((co & 2) << 3));
+}
+
+__global__ __launch_bounds__(FT, 1) void f32_conv_bwd_kernel(
+    const float* __restrict__ a1g, const float* __restrict__ xng, const float* __restrict__ dpool,
+    const uint8_t* __restrict__ pmask, const float* __restrict__ w2, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) char smem[CB_TOTAL];
+  float* xs = reinterpret_cast<float*>(smem + CB_XS);
+  float* a1 = reinterpret_cast<float*>(smem + CB_A1);
+  float* dz = reinterpret_cast<float*>(smem + CB_DZ);
+  float* w2t = reinterpret_cast<float*>(smem + CB_W2);
+  const int img = blockIdx.x / CB_S, band = blockIdx.x - img * CB_S;
+  const int d0 = band * CB_R;
+  const int aown = band == CB_S - 1 ? CB_R + 2 : CB_R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  float* out = slab + (int64_t)blockIdx.x * CNN_CONV_SLAB;
+  // ---- staging: zero dz2, x / a1 rows, W2^T
+  for (int i = tid; i < (2 + CB_ZR * H1) * DZS / 4; i += FT)
+    reinterpret_cast<float4*>(dz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < (CB_R + 4) * IMG; i += FT)
+    xs[i] = xng[(int64_t)img * 784 + d0 * IMG + i];
+  for (int i = tid; i < (CB_R + 2) * H1 * C1; i += FT) {
+    const int p = i >> 5, c = i & 31;
+    a1[p * A1S + c] = a1g[((int64_t)img * P1 + d0 * H1) * C1 + i];
+  }
+  for (int e = tid; e < C2 * 288; e += FT) {
+    const int co = e / 288, k = e - co * 288;
+    w2t[w2t_off(k >> 5, co, k & 31)] = w2[e];
+  }
+  __syncthreads();
+  // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (halo row above included) + db2 of the
+  // band's own pooled rows; thread -> fixed channel co = tid & 63
+  const int pr0 = band == 0 ? 0 : d0 / 2 - 1;
+  const int npr = d0 / 2 + CB_R / 2 - pr0;
+  float db2p = 0.f;
+  for (int it = tid; it < npr * HP * C2; it += FT) {
+    const int pl = it >> 6, co = it & 63;
+    const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
+    const int gi = (py * HP + px) * C2 + co;
+    const uint8_t mk = pmask[(int64_t)img * FEAT + gi];
+    if (mk & 0x80) {
+      const float v = dpool[(int64_t)img * FEAT + gi];
+      const int sidx = __builtin_ctz((unsigned)mk & 0xf);
+      const int lr = 2 * py + (sidx >> 1) - (d0 - 2);   // local dz2 row
+      dz[(2 + lr * H1 + 2 * px + (sidx & 1)) * DZS + co] = v;
+      if (py >= d0 / 2) db2p += v;
+    }
+  }
+  __syncthreads();
+  // ---- conv2 dgrad over the band's own a1 pixels (m-tiles of 16 pixels p = 26 y + x, N = 32
+  // ci, K = 9 taps x 64 co) + relu'(a1) + conv1 weight/bias gradient on the fp32 MFMA:
+  // dW1[ci][tap] += sum_p dz1[p][ci] x[p + tap]; the dgrad accumulator (rows = pixels, cols = ci)
+  // already is its A operand (M = ci, K = pixel), the B operand is x (N = tap, 9 = bias ones)
+  f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int npx = aown * H1, nmt = (npx + 15) / 16;
+  for (int mt = wave; mt < nmt; mt += 8) {
+    const int p = min(mt * 16 + i16, npx - 1);           // A row: this lane's pixel
+    const int y = p / H1, x = p - y * H1;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const float* ap = dz + (2 + (y + 2 - ky) * H1 + x - kx) * DZS + g;
+#pragma unroll
+      for (int c16 = 0; c16 < 16; ++c16) {
+        const float av = ap[c16 * 4];
+        const int co = c16 * 4 + g;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma4(av, w2t[w2t_off(tap, co, nt * 16 + i16)], acc[nt]);
+      }
+    }
+    // epilogue: lane holds da1 of pixels mt * 16 + 4 g + r, channel nt * 16 + i16
+    float xb[4];
+    const int ctap = i16;                                  // conv1-wgrad column: tap / bias
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pr = mt * 16 + 4 * g + r;
+      const int yy = pr / H1, xx = pr - yy * H1;
+      const bool valid = pr < npx;
+      xb[r] = !valid ? 0.f
+              : ctap < 9 ? xs[(yy + ctap / 3) * IMG + xx + ctap % 3]
+              : ctap == 9 ? 1.f : 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const float a1v = valid ? a1[min(pr, npx - 1) * A1S + nt * 16 + i16] : 0.f;
+        acc[nt][r] = (valid && a1v > 0.f) ? acc[nt][r] : 0.f;   // dz1 = da1 relu'(a1)
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
+  }
+  // ---- conv2 wgrad over the band's own dz2 rows: tiles (co tile, tap x ci tile) = 4 x 18,
+  // K = 4 rows x 24 columns (k-steps of 4 pixels of one row)
+  for (int t = wave; t < 72; t += 8) {
+    const int mt = t / 18, nn = t - mt * 18;
+    const int tap = nn >> 1, ct = nn & 1;
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < CB_R * 6; ++ks) {
+      const int rr = ks / 6, c0 = (ks - rr * 6) * 4;
+      const float av = dz[(2 + (rr + 2) * H1 + c0 + g) * DZS + mt * 16 + i16];
+      const float bv = a1[((rr + ky) * H1 + c0 + g + kx) * A1S + ct * 16 + i16];
+      acc = mfma4(av, bv, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16] = acc[r];
+  }
+  __syncthreads();   // dz2 region free: reduction scratch
+  float* red = dz;
+  // conv1 partials acc1[nt]: rows ci = nt * 16 + 4 g + r, column tap = i16
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave * 512 + (nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
+  red[4096 + tid] = db2p;
+  __syncthreads();
+  if (tid < C2) {
+    float sacc = 0.f;
+    for (int w = 0; w < 8; ++w) sacc += red[4096 + w * 64 + tid];
+    out[SLB_DB2 + tid] = sacc;
+  } else if (tid >= 64 && tid < 64 + C1 * 10) {
+    const int e = tid - 64, ci = e / 10, tp = e - 10 * ci;
+    float sacc = 0.f;
+    for (int w = 0; w < 8; ++w) sacc += red[w * 512 + ci * 16 + tp];
+    if (tp < 9) out[SLB_DW1 + ci * 9 + tp] = sacc;
+    else out[SLB_DB1 + ci] = sacc;
+  }
+}
+
+}  // namespace
+
+void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
+                    int bfull, int B, const float* w1, const float* b1, const float* w2,
+                    const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
+                    int32_t* ylab, hipStream_t st) {
+  if (a1g != nullptr)
+    f32_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, bfull, w1, b1, w2, b2, pool,
+                                           pmask, a1g, xng, ylab);
+  else
+    f32_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, bfull, w1, b1, w2, b2, pool,
+                                            pmask, a1g, xng, ylab);
+}
+
+void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,
+                        hipStream_t st) {
+  f32_fc1_fwd_kernel<<<((B + 31) / 32) * splitk, 256, 0, st>>>(pool, w1, part, B, FEAT / splitk);
+}
+
+void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
+                        float* gwf1, float* dpool, const float* head_slab, int head_blocks,
+                        float* gwf2, float* gbf2, float* gbf1, double* metrics, hipStream_t st) {
+  const int nblk = DW_T + (ldt / 32) * DX_T + HRB;
+  f32_fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, ldt, pool, w1, B, gwf1, dpool, head_slab,
+                                           head_blocks, gwf2, gbf2, gbf1, metrics);
+}
+
+int f32_conv_bwd_blocks(int B) { return B * CB_S; }
+
+void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
+                         const uint8_t* pmask, const float* w2, int B, float* slab, hipStream_t st) {
+  f32_conv_bwd_kernel<<<B * CB_S, FT, 0, st>>>(a1g, xng, dpool, pmask, w2, slab);
+}

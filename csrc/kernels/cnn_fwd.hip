@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
     const float* __restrict__ part, int S, int B, const float* __restrict__ bf1,
     const float* __restrict__ wf2, const float* __restrict__ bf2, const int32_t* __restrict__ ylab,
     bf16* __restrict__ dh, bf16* __restrict__ dht, int ldt, float* __restrict__ slab,
-    double* __restrict__ metrics, int64_t* c0, int64_t* c1, unsigned* c2) {
+    double* __restrict__ metrics, int64_t* c0, int64_t* c1, unsigned* c2, float* __restrict__ dh32) {
   static_assert(HEAD_ROWS == 4, "one wave per row, 4 waves");
   __shared__ float hs[HEAD_ROWS][HID];
   __shared__ float dhs[HEAD_ROWS][HID];
@@ -475,12 +475,17 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
       dhv.x = h.x > 0.f ? dhv.x : 0.f;
       dhv.y = h.y > 0.f ? dhv.y : 0.f;
       // row < ldt always: rows >= B write zeros (GEMM padding)
-      const bf16x2 o = {to_bf16(dhv.x), to_bf16(dhv.y)};
-      // both copies fragment-major (kernels.h frag_pos), the layouts fc1_bwd's dW (dh^T: m =
-      // hidden unit, k = batch row) and dX (dh: m = batch row, k = hidden unit) tiles load
-      dht[frag_pos(2 * j, row, ldt)] = o[0];
-      dht[frag_pos(2 * j + 1, row, ldt)] = o[1];
-      *reinterpret_cast<bf16x2*>(dh + frag_pos(row, 2 * j, HID)) = o;
+      if (dh32 != nullptr) {
+        // fp32 step (cnn_f32.hip): dh row-major in fp32 (rows >= B are zero, GEMM padding)
+        reinterpret_cast<float2*>(dh32 + (int64_t)row * HID)[j] = dhv;
+      } else {
+        const bf16x2 o = {to_bf16(dhv.x), to_bf16(dhv.y)};
+        // both copies fragment-major (kernels.h frag_pos), the layouts fc1_bwd's dW (dh^T: m =
+        // hidden unit, k = batch row) and dX (dh: m = batch row, k = hidden unit) tiles load
+        dht[frag_pos(2 * j, row, ldt)] = o[0];
+        dht[frag_pos(2 * j + 1, row, ldt)] = o[1];
+        *reinterpret_cast<bf16x2*>(dh + frag_pos(row, 2 * j, HID)) = o;
+      }
       reinterpret_cast<float2*>(hs[r])[j] = h;
       reinterpret_cast<float2*>(dhs[r])[j] = dhv;
       if (j == 0) {
@@ -564,15 +569,15 @@ void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, i
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
-                     unsigned* c2, hipStream_t st) {
+                     unsigned* c2, float* dh32, hipStream_t st) {
   const int groups = (train ? ldt : B + HEAD_ROWS - 1) / HEAD_ROWS;
   const int nblk = cnn_head_blocks(groups);
   if (train)
     cnn_head_kernel<true><<<nblk, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh, dht, ldt,
-                                                slab, metrics, c0, c1, c2);
+                                                slab, metrics, c0, c1, c2, dh32);
   else
     cnn_head_kernel<false><<<nblk, 256, 0, st>>>(part, splitk, B, bf1, wf2, bf2, ylab, dh, dht,
-                                                 ldt, slab, metrics, c0, c1, c2);
+                                                 ldt, slab, metrics, c0, c1, c2, dh32);
 }
 
 int cnn_head_blocks(int groups) { return groups < CNN_HEAD_MAX_BLOCKS ? groups : CNN_HEAD_MAX_BLOCKS; }

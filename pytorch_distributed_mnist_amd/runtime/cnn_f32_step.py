@@ -1,0 +1,148 @@
+"""CNN fp32 GPU step program (``--arch cnn --dtype fp32``): the reference's precision.
+
+The reference trains in fp32 (``multi_proc_single_gpu.py:185-191``).  Same chain as the bf16
+program (``cnn_step.py``), on the fp32 matrix cores (``csrc/kernels/cnn_f32.hip``,
+``v_mfma_f32_16x16x4_f32``), reading the fp32 master weights directly (no bf16 copies):
+
+  f32_fwd      gather-free epoch buffer row, normalise, conv1 + ReLU, conv2 + ReLU + maxpool
+               -> pool, mask; a1 and the normalised x for the backward
+  f32_fc1_fwd  split-K fc1 GEMM -> fp32 partials
+  cnn_head     fc1 reduce + bias + ReLU, fc2, CE, head backward (dh in fp32), counters
+  f32_fc1_bwd  dW1 tiles | dX tiles | head-slab reduction           -> bucket 0 complete
+  f32_conv_bwd conv2 dgrad + relu' + conv1 wgrad, conv2 wgrad       -> conv slabs
+  world_size 1: optimizer with the conv slab reduction fused in
+  world_size>1: conv_reduce -> all-reduce (both buckets) -> optimizer
+"""
+from __future__ import annotations
+
+import torch
+
+from .gpu_step import GpuStepBase
+
+EVAL_CHUNK = 2048
+SPLITK_TRAIN = 32        # fc1 split-K (divides 288: whole 32-float k chunks per split)
+
+
+def splitk_eval(b: int) -> int:
+    """Split-K for an eval chunk of b rows: ~256 fc1 workgroups."""
+    mt = -(-b // 32)
+    for s in (32, 16, 8, 4, 2, 1):
+        if mt * s <= 256:
+            return s
+    return 1
+
+
+class CnnStepF32(GpuStepBase):
+    CONV = ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")
+
+    def __init__(self, prog, use_graphs):
+        super().__init__(prog, use_graphs)
+        C, dev, B = self.C, self.device, self.bfull
+        f32 = torch.float32
+        self.ldt = -(-B // 32) * 32
+        cap = max(B, EVAL_CHUNK)
+        self.pool = torch.empty(cap * 9216, dtype=f32, device=dev)
+        self.pmask = torch.empty(B * 9216, dtype=torch.uint8, device=dev)
+        self.a1g = torch.empty(B * 676 * 32, dtype=f32, device=dev)
+        self.xng = torch.empty(B * 784, dtype=f32, device=dev)
+        self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
+        part_n = max(SPLITK_TRAIN * B, splitk_eval(EVAL_CHUNK) * EVAL_CHUNK) * 128
+        self.part = torch.empty(part_n, dtype=f32, device=dev)
+        self.dh32 = torch.zeros(self.ldt * 128, dtype=f32, device=dev)
+        self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=f32,
+                                     device=dev)
+        self.dpool = torch.empty(B * 9216, dtype=f32, device=dev)
+        self.conv_slab = torch.empty(C.f32_conv_bwd_nblk(B) * C.CNN_CONV_SLAB, dtype=f32,
+                                     device=dev)
+        a = self.arena
+        self.P = {n: a.param(n) for n in ("conv1.weight", "conv1.bias", "conv2.weight",
+                                          "conv2.bias", "fc1.weight", "fc1.bias", "fc2.weight",
+                                          "fc2.bias")}
+        self.G = {n: a.grad(n) for n in self.P}
+        self.fuse_conv_reduce = not self.reducer.active
+        if getattr(self.reducer, "streamed", False):
+            # the persistent (streamed) xgmi collective is wired into the bf16 kernels' device
+            # hand-off words; the fp32 program uses the transport's per-bucket launches
+            self.reducer.streamed = False
+        self._fused = {}
+        self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
+
+    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
+        n = idx_cpu.numel()
+        if self.ep_images.numel() != n * 784:
+            self.ep_images = torch.empty(n * 784, dtype=torch.uint8, device=self.device)
+            self.ep_labels = torch.empty(n, dtype=torch.int32, device=self.device)
+            self.graphs.clear()
+        super().set_train_indices(idx_cpu)
+        self.C.gather_epoch(self.train_images, self.train_labels, self.idx,
+                            self.ep_images.view(n, 784), self.ep_labels)
+
+    def refresh_shadows(self) -> None:
+        """No bf16 operand copies in the fp32 program."""
+
+    def optimizer_segments(self):
+        spec = self.arena.spec
+        return [(spec.offset(p.name), 1, p.numel, None, None) for p in spec.params]
+
+    def invalidate_graphs(self) -> None:
+        super().invalidate_graphs()
+        self._fused = {}
+
+    def _fused_segments(self, nblk: int):
+        """Segments whose conv gradients are the fixed-order sum of `nblk` conv slabs."""
+        segs = self._fused.get(nblk)
+        if segs is None:
+            C, spec = self.C, self.arena.spec
+            col = {"conv2.weight": 0, "conv2.bias": C.CNN_CONV_SLAB_DB2,
+                   "conv1.weight": C.CNN_CONV_SLAB_DW1, "conv1.bias": C.CNN_CONV_SLAB_DB1}
+            slab_segs, plain = [], []
+            for p in spec.params:
+                sg = (spec.offset(p.name), 1, p.numel, None, None)
+                if p.name in col:
+                    slab_segs.append(sg + ((self.conv_slab, nblk, col[p.name], C.CNN_CONV_SLAB),))
+                else:
+                    plain.append(sg)
+            segs = slab_segs + plain
+            self._fused[nblk] = segs
+        return segs
+
+    def _train_impl(self, B: int) -> None:
+        C, P, G = self.C, self.P, self.G
+        ldt = -(-B // 32) * 32
+        C.f32_fwd(self.ep_images.view(-1, 784), self.ep_labels, self.ctr[0:1], self.bfull, B,
+                  P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
+                  self.pool, self.pmask, self.a1g, self.xng, self.ylab)
+        C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN)
+        C.cnn_head(self.part, SPLITK_TRAIN, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
+                   self.ylab, True, None, None, ldt, self.head_slab, self.metrics.train_view(),
+                   self.ctr[0:1], self.opt._step_dev, None, self.dh32)
+        C.f32_fc1_bwd(self.dh32, ldt, self.pool, P["fc1.weight"], B, G["fc1.weight"], self.dpool,
+                      self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
+                      self.metrics.train_view())
+        red = self.reducer
+        red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
+        C.f32_conv_bwd(self.a1g, self.xng, self.dpool, self.pmask, P["conv2.weight"], B,
+                       self.conv_slab)
+        nblk = C.f32_conv_bwd_nblk(B)
+        if self.fuse_conv_reduce:
+            self.launch_optimizer(self._fused_segments(nblk))
+            return
+        C.conv_reduce(self.conv_slab, nblk, G["conv2.weight"], G["conv2.bias"],
+                      G["conv1.weight"], G["conv1.bias"])
+        red.bucket_ready(1)
+        red.finalize()
+        self.launch_optimizer()
+
+    def evaluate(self) -> None:
+        C, P = self.C, self.P
+        n = self.test_images.shape[0]
+        for s in range(0, n, EVAL_CHUNK):
+            b = min(EVAL_CHUNK, n - s)
+            se = splitk_eval(b)
+            C.f32_fwd(self.test_images[s:s + b], self.test_labels[s:s + b], None, b, b,
+                      P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
+                      self.pool, None, None, None, self.ylab)
+            C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, b, se)
+            C.cnn_head(self.part, se, b, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
+                       False, None, None, 32, None, self.metrics.eval_view(), None, None)

@@ -30,8 +30,11 @@ def make_gpu_step(prog, use_graphs: bool = True):
             raise ValueError("the reference Linear model runs in fp32 (--dtype fp32)")
         return LinearStep(prog, use_graphs)
     if prog.model == "cnn":
+        if prog.dtype == "fp32":                 # the reference's precision, fp32 MFMA
+            from .cnn_f32_step import CnnStepF32
+            return CnnStepF32(prog, use_graphs)
         if prog.dtype != "bf16":
-            raise ValueError("the CNN GPU path computes in bf16 (--dtype bf16)")
+            raise ValueError(f"unsupported CNN dtype {prog.dtype!r} (bf16 or fp32)")
         from .cnn_step import CnnStep
         return CnnStep(prog, use_graphs)
     raise ValueError(prog.model)

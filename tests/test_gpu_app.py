@@ -87,3 +87,33 @@ def test_two_ranks_on_one_gpu_match_one_rank(gpu, tmp_path, monkeypatch):
     for k in a:
         err = ((a[k] - b[k]).norm() / a[k].norm()).item()
         assert err < 2e-2, (k, err)
+
+
+def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path):
+    """--arch cnn --dtype fp32 (the reference's precision, fp32 MFMA kernels): train, resume,
+    evaluate on the GPU, and the same run on the CPU path: every printed loss agrees to fp32
+    summation noise (the bf16 path agrees only to bf16 accuracy)."""
+    d1, d2 = tmp_path / "gpu", tmp_path / "cpu"
+    d1.mkdir()
+    d2.mkdir()
+    common = ["--arch", "cnn", "--optimizer", "sgd", "--lr", "0.05", "--dtype", "fp32",
+              "--synthetic-size", "2048", "--epochs", "2", "--seed", "4"]
+    g = [l for l in cli(common, d1) if l.startswith("Epoch:")]
+    c = [l for l in cli(common, d2, device="cpu", backend="gloo") if l.startswith("Epoch:")]
+    assert len(g) == len(c) == 2
+    for lg, lc in zip(g, c):
+        mg, mc = EPOCH_RE.match(lg), EPOCH_RE.match(lc)
+        for i in (3, 5):
+            assert abs(float(mg.group(i)) - float(mc.group(i))) < 5e-5, (lg, lc)
+        for i in (4, 6):
+            assert abs(float(mg.group(i)) - float(mc.group(i))) <= 0.1, (lg, lc)
+    ck = d1 / "checkpoints" / "checkpoint_1.pth.tar"
+    ev = [l for l in cli(["--arch", "cnn", "--optimizer", "sgd", "--dtype", "fp32", "--evaluate",
+                          "--resume", str(ck)], d1) if l.startswith("test loss:")]
+    m = EPOCH_RE.match(g[1])
+    assert ev == ["test loss: {}, test acc: {}%.".format(m.group(5), m.group(6))]
+    # resume continues at epoch 2
+    r = [l for l in cli(["--arch", "cnn", "--optimizer", "sgd", "--lr", "0.05", "--dtype", "fp32",
+                         "--synthetic-size", "2048", "--epochs", "3", "--resume", str(ck)], d1)
+         if l.startswith("Epoch:")]
+    assert len(r) == 1 and r[0].startswith("Epoch: 2/3,")

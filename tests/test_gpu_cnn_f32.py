@@ -1,0 +1,121 @@
+"""CNN fp32 GPU path (``--dtype fp32``, cnn_f32.hip on v_mfma_f32_16x16x4_f32) against fp32
+PyTorch autograd: the reference trains in fp32 (multi_proc_single_gpu.py:185-191), so the
+gradients of one step must agree to fp32 summation-order noise (<= 1e-4 relative)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_mnist_amd.data.mnist import normalize_reference, synthetic_split
+from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+from pytorch_distributed_mnist_amd.models.reference import MODULES
+from pytorch_distributed_mnist_amd.runtime.program import build_local_program
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _program(B, n, lr=0.0, graphs=False, seed=0, optimizer="sgd"):
+    train = synthetic_split(n, True)
+    test = synthetic_split(300, False)
+    prog = build_local_program("cnn", "fp32", "cuda", B, train, test, optimizer=optimizer, lr=lr,
+                               momentum=0.0 if lr == 0.0 else 0.9,
+                               weight_decay=0.0 if lr == 0.0 else 1e-4, seed=seed,
+                               use_graphs=graphs)
+    prog.optimizer.sync_hyperparams()
+    return prog, train, test
+
+
+def _reference_net(prog):
+    net = MODULES["cnn"]()
+    sd = {k[len("module."):]: v for k, v in prog.arena.state_dict().items()}
+    net.load_state_dict(sd)
+    return net
+
+
+@pytest.mark.parametrize("B", [64, 37, 256])
+def test_f32_gradients_match_fp32_autograd(gpu, B):
+    """One training step with lr = 0: the gradient arena holds the step's gradients (the fused
+    optimizer writes the reduced conv gradients back), compared per parameter with autograd."""
+    prog, train, _ = _program(B, n=max(2 * B, 300))
+    idx = distributed_indices(len(train), 1, 0, 0)
+    prog.set_train_indices(idx)
+    net = _reference_net(prog)
+    prog.gpu.begin_epoch()
+    prog.gpu.train_step(B)
+    torch.cuda.synchronize()
+    sel = idx[:B]
+    x = normalize_reference(train.images[sel]).view(B, 1, 28, 28)
+    out = net(x)
+    loss = F.cross_entropy(out, train.labels[sel])
+    loss.backward()
+    # fp64 autograd of the same step: the yardstick for both fp32 implementations (the conv1
+    # weight gradient sums ~B * 676 terms with heavy cancellation, so fp32 results differ from
+    # each other by more than from fp64)
+    net64 = _reference_net(prog).double()
+    F.cross_entropy(net64(x.double()), train.labels[sel]).backward()
+    ref64 = dict(net64.named_parameters())
+    got = prog.arena.torch_tensors(prog.arena.grads)
+    for name, p in net.named_parameters():
+        r64 = rel(got[name].double(), ref64[name].grad)
+        t64 = rel(p.grad.double(), ref64[name].grad)
+        r32 = rel(got[name], p.grad)
+        assert r64 < max(1e-4, 2 * t64) and r32 < 1e-3, (name, r64, t64, r32)
+    tl = prog.metrics.buf[0].item()
+    assert abs(tl - loss.item() * B) <= 1e-4 * B
+    correct = (out.argmax(1) == train.labels[sel]).sum().item()
+    assert prog.metrics.buf[1].item() == correct
+
+
+def test_f32_training_tracks_cpu_sgd(gpu):
+    """Several SGD-momentum steps (graph-captured) stay within fp32 noise of the same steps
+    in torch on the CPU, and the evaluation matches."""
+    B = 64
+    prog, train, test = _program(B, n=B * 5, lr=0.05, graphs=True, seed=3)
+    idx = distributed_indices(len(train), 1, 0, 0)
+    net = _reference_net(prog)
+    opt = torch.optim.SGD(net.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    prog.set_train_indices(idx)
+    prog.train_epoch()
+    torch.cuda.synchronize()
+    for s in range(5):
+        sel = idx[s * B:(s + 1) * B]
+        opt.zero_grad()
+        F.cross_entropy(net(normalize_reference(train.images[sel]).view(B, 1, 28, 28)),
+                        train.labels[sel]).backward()
+        opt.step()
+    got = prog.arena.state_dict()
+    for name, p in net.named_parameters():
+        r = rel(got["module." + name], p.detach())
+        assert r < 1e-4, (name, r)
+    tl, ta = prog.evaluate()
+    with torch.no_grad():
+        out = net(normalize_reference(test.images).view(-1, 1, 28, 28))
+        ref_loss = F.cross_entropy(out, test.labels).item()
+        ref_acc = (out.argmax(1) == test.labels).float().mean().item()
+    assert abs(tl.average - ref_loss) < 1e-4 * max(1.0, ref_loss)
+    assert abs(ta.accuracy - ref_acc) < 1e-6 + 2.0 / len(test.labels)
+
+
+def test_f32_ws2_structure_matches_local(gpu):
+    """The world-size>1 chain (conv_reduce, bucket all-reduce through a 1-rank RCCL
+    communicator, one optimizer launch) gives the same parameters as the fused local chain."""
+    from pytorch_distributed_mnist_amd.parallel.comm import RcclComm
+    train = synthetic_split(64 * 4, True)
+    test = synthetic_split(64, False)
+    out = []
+    for force in (False, True):
+        comm = RcclComm(0, 1, gpu) if force else None
+        p = build_local_program("cnn", "fp32", "cuda", 64, train, test, optimizer="sgd", lr=0.05,
+                                momentum=0.9, seed=5, use_graphs=True, comm=comm,
+                                force_comm=force, transport="rccl")
+        p.optimizer.sync_hyperparams()
+        p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        p.train_epoch()
+        torch.cuda.synchronize()
+        out.append(p.arena.params.clone())
+        if comm is not None:
+            comm.close()
+    assert torch.equal(out[0], out[1])

@@ -18,7 +18,13 @@ network), so this tool reproduces its per-step behaviour with plain PyTorch:
     python -m torch.distributed.run --nproc-per-node N ... tools/reference_eager.py
 
 `--loader device` swaps the DataLoader for device-resident normalised tensors indexed per
-step (a stronger eager baseline than the reference's own data path).  Prints one JSON line.
+step (a stronger eager baseline than the reference's own data path).  `--loader graph` is the
+strongest plain-PyTorch version of the same step: device-resident data, the batch gathered by a
+device-side step counter, no per-step .item() (loss / correct accumulated on the device), the
+whole step (gather, forward, loss, backward, SGD/Adam) captured once into a torch.cuda.graph
+(hipGraph) and replayed; `--amp bf16` runs it under torch.autocast(bfloat16) with fp32
+master weights (this framework's bf16 configuration).  With --loader graph the single-GPU run
+uses no DDP wrapper (nothing to reduce).  Prints one JSON line.
 """
 from __future__ import annotations
 
@@ -61,7 +67,9 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--model", choices=["cnn", "linear"], default="cnn")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
-    ap.add_argument("--loader", choices=["dataloader", "device"], default="dataloader")
+    ap.add_argument("--loader", choices=["dataloader", "device", "graph"], default="dataloader")
+    ap.add_argument("--amp", choices=["none", "bf16"], default="none",
+                    help="--loader graph: torch.autocast(bfloat16) over forward + loss")
     ap.add_argument("--train-size", type=int, default=60000)
     a = ap.parse_args()
 
@@ -76,6 +84,8 @@ def main():
 
     torch.manual_seed(1234)
     model = (CNN() if a.model == "cnn" else Net()).to(dev)
+    if a.loader == "graph":
+        return graph_loop(a, model, dev, rank, ws)
     model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank])
     if a.optimizer == "sgd":
         opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
@@ -149,6 +159,83 @@ def main():
             "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 4),
             "images_per_sec": round(total / el, 1),
+        }), flush=True)
+    dist.destroy_process_group()
+
+
+def graph_loop(a, model, dev, rank, ws):
+    """Device-resident data + whole-step torch.cuda.graph capture (+ optional bf16 autocast)."""
+    if ws > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+    if a.optimizer == "sgd":
+        opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
+    split = synthetic_split(a.train_size, True)
+    x_dev = ((split.images.to(dev).float() / 255.0 - 0.1307) / 0.3081).view(-1, 1, 28, 28)
+    y_dev = split.labels.to(dev)
+    n = x_dev.shape[0]
+    per_rank = n // ws
+    steps_per_epoch = per_rank // a.batch
+    g = torch.Generator(device="cpu")
+    g.manual_seed(0)
+    perm = torch.randperm(n, generator=g)[rank:per_rank * ws:ws].to(dev)   # DistributedSampler-like
+    ctr = torch.zeros((), dtype=torch.long, device=dev)
+    ar = torch.arange(a.batch, device=dev)
+    loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
+    correct = torch.zeros((), dtype=torch.long, device=dev)
+    amp = a.amp == "bf16"
+
+    def step():
+        idx = perm[(ctr % steps_per_epoch) * a.batch + ar]
+        x, y = x_dev[idx], y_dev[idx]
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = model(x)
+            loss = F.cross_entropy(out, y)
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        opt.step()
+        loss_sum.add_(loss.detach().float() * a.batch)
+        correct.add_(out.argmax(1).eq(y).sum())
+        ctr.add_(1)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):                 # warm up (optimizer state, autograd buffers)
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    opt.zero_grad(set_to_none=False)
+    with torch.cuda.graph(graph):
+        step()
+    for _ in range(a.warmup):
+        graph.replay()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if ws > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    if rank == 0:
+        print(json.dumps({
+            "what": "the same CNN step in PyTorch: device-resident data, whole step captured in "
+                    "a torch.cuda.graph" + (", bf16 autocast" if amp else ", fp32"),
+            "model": a.model, "optimizer": a.optimizer, "loader": "graph", "amp": a.amp,
+            "n_gpus": ws, "batch_per_rank": a.batch, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 4),
+            "images_per_sec": round(a.steps * a.batch * ws / el, 1),
+            "train_loss_mean": round(float(loss_sum.item()) / max(1, int(ctr.item()) * a.batch), 4),
         }), flush=True)
     dist.destroy_process_group()
 
