@@ -35,10 +35,33 @@ def _reference_net(prog):
     return net
 
 
+def _fp64_grads_with_mask(prog, x, y, pmask, B):
+    """fp64 autograd of the step, max-pool routed by the kernel's own argmax decisions (the
+    pool mask): where two window values tie within fp32 rounding, fp32 and fp64 may pick
+    different positions, and a gradient routed to a neighbouring pixel is a discrete
+    difference, not a precision one."""
+    net = _reference_net(prog).double()
+    a1 = F.relu(net.conv1(x.double()))
+    z2 = net.conv2(a1)                                            # [B, 64, 24, 24]
+    mk = pmask[:B * 9216].view(B, 12, 12, 64).permute(0, 3, 1, 2).cpu().long()
+    pos = (mk & 0x80) != 0
+    sidx = torch.where(pos, (mk & 0xf).float().log2().long(), torch.zeros_like(mk))
+    py = torch.arange(12).view(1, 1, 12, 1)
+    px = torch.arange(12).view(1, 1, 1, 12)
+    flat = (2 * py + (sidx >> 1)) * 24 + 2 * px + (sidx & 1)
+    pooled = torch.where(pos, z2.flatten(2).gather(2, flat.flatten(2)).view(B, 64, 12, 12),
+                         torch.zeros((), dtype=torch.float64))
+    out = net.fc2(F.relu(net.fc1(pooled.flatten(1))))
+    F.cross_entropy(out, y).backward()
+    return dict(net.named_parameters()), out
+
+
 @pytest.mark.parametrize("B", [64, 37, 256])
 def test_f32_gradients_match_fp32_autograd(gpu, B):
     """One training step with lr = 0: the gradient arena holds the step's gradients (the fused
-    optimizer writes the reduced conv gradients back), compared per parameter with autograd."""
+    optimizer writes the reduced conv gradients back).  Compared per parameter with fp64
+    autograd of the same step (max-pool routed as the kernel routed it): <= 1e-4 relative,
+    fp32 summation-order noise; and with fp32 autograd (torch's own routing)."""
     prog, train, _ = _program(B, n=max(2 * B, 300))
     idx = distributed_indices(len(train), 1, 0, 0)
     prog.set_train_indices(idx)
@@ -51,18 +74,13 @@ def test_f32_gradients_match_fp32_autograd(gpu, B):
     out = net(x)
     loss = F.cross_entropy(out, train.labels[sel])
     loss.backward()
-    # fp64 autograd of the same step: the yardstick for both fp32 implementations (the conv1
-    # weight gradient sums ~B * 676 terms with heavy cancellation, so fp32 results differ from
-    # each other by more than from fp64)
-    net64 = _reference_net(prog).double()
-    F.cross_entropy(net64(x.double()), train.labels[sel]).backward()
-    ref64 = dict(net64.named_parameters())
+    ref64, _ = _fp64_grads_with_mask(prog, x, train.labels[sel], prog.gpu.pmask, B)
     got = prog.arena.torch_tensors(prog.arena.grads)
     for name, p in net.named_parameters():
         r64 = rel(got[name].double(), ref64[name].grad)
-        t64 = rel(p.grad.double(), ref64[name].grad)
-        r32 = rel(got[name], p.grad)
-        assert r64 < max(1e-4, 2 * t64) and r32 < 1e-3, (name, r64, t64, r32)
+        assert r64 < 1e-4, (name, r64)
+        if not name.startswith("conv"):        # the conv gradients see any argmax tie flip
+            assert rel(got[name], p.grad) < 1e-4, name
     tl = prog.metrics.buf[0].item()
     assert abs(tl - loss.item() * B) <= 1e-4 * B
     correct = (out.argmax(1) == train.labels[sel]).sum().item()
