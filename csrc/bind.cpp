@@ -392,11 +392,12 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
   const int64_t* pctr = counted ? ctr->data_ptr<int64_t>() : nullptr;
   uint8_t* pxg = train ? xg->data_ptr<uint8_t>() : nullptr;
   if (bands > 1) {
-    // training: the band backward's inputs (a1 image + normalised x) instead of the uint8 x
+    // training: the band backward's inputs (a1 image + normalised x: a1g, xng) and / or the
+    // one-image backward's uint8 image (xg)
     __bf16* pa1 = nullptr;
     __bf16* pxn = nullptr;
-    if (train) {
-      TORCH_CHECK(a1g.has_value() && xng.has_value(), "band training needs a1g and xng");
+    if (a1g.has_value() && a1g->defined()) {
+      TORCH_CHECK(xng.has_value() && xng->defined(), "a1g needs xng");
       need_min(*a1g, at::kBFloat16, B * 676 * 32, "a1g");
       need_min(*xng, at::kBFloat16, B * 784, "xng");
       need_aligned(a1g->data_ptr(), 16, "a1g");
@@ -407,7 +408,7 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
     launch_cnn_fwd_band(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
                         (int)bfull, (int)B, (int)bands, w1.data_ptr<float>(), b1.data_ptr<float>(),
                         ptr<__bf16>(w2), b2.data_ptr<float>(), ptr<__bf16>(pool),
-                        pmask.data_ptr<uint8_t>(), pa1, pxn, ylab.data_ptr<int32_t>(),
+                        pmask.data_ptr<uint8_t>(), pa1, pxn, pxg, ylab.data_ptr<int32_t>(),
                         cur_stream(images));
   } else {
     launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
@@ -472,14 +473,15 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
 }
 
 // fc_update (world size 1, optional): (kind, p, g, m, v or None, shadow, lr, step, beta1,
-// beta2, eps, wd, momentum, dampening, nesterov, grad_scale) -- the fc1-weight update of the
-// optimizer, run by cnn_bwd (kernels.h FcUpdate)
+// beta2, eps, wd, momentum, dampening, nesterov, grad_scale[, shadow_t2]) -- the fc1-weight
+// update of the optimizer, run by fc1_bwd (kernels.h FcUpdate); shadow_t2 (2 x W1^T, the
+// tensor passed as wf1t) double-buffers the transposed copy
 static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   FcUpdate u{};
   u.kind = -1;
   if (!t.has_value()) return u;
   const py::tuple& a = *t;
-  TORCH_CHECK(a.size() == 16, "fc_update: 16 entries");
+  TORCH_CHECK(a.size() == 16 || a.size() == 17, "fc_update: 16 or 17 entries");
   u.kind = (int)a[0].cast<int64_t>();
   TORCH_CHECK(u.kind == OPT_SGD, "fc_update: SGD-momentum only (Adam runs in the optimizer kernel)");
   auto p = a[1].cast<at::Tensor>(), g = a[2].cast<at::Tensor>(), m = a[3].cast<at::Tensor>();
@@ -512,6 +514,14 @@ static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   u.dampening = (float)a[13].cast<double>();
   u.nesterov = a[14].cast<bool>() ? 1 : 0;
   u.grad_scale = (float)a[15].cast<double>();
+  u.shadow_t2 = nullptr;
+  if (a.size() == 17 && !a[16].is_none()) {
+    auto t2 = a[16].cast<at::Tensor>();
+    need(t2, at::kBFloat16, "fc shadow_t2");
+    TORCH_CHECK(t2.numel() == 2 * u.numel, "fc_update: shadow_t2 holds two W1^T copies");
+    need_aligned(t2.data_ptr(), 16, "fc_update shadow_t2");
+    u.shadow_t2 = ptr<__bf16>(t2);
+  }
   return u;
 }
 
@@ -536,10 +546,13 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
   need_min(head_slab, at::kFloat, hb * CNN_HEAD_SLAB, "head slab");
   need(metrics, at::kDouble, "metrics");
   need_numel(metrics, 3, "metrics");
+  const FcUpdate fcu = make_fc_update(fc_update);
+  TORCH_CHECK(fcu.shadow_t2 == nullptr || fcu.shadow_t2 == ptr<__bf16>(wf1t),
+              "fc_update: shadow_t2 must be the wf1t double buffer");
   launch_fc1_bwd(ptr<__bf16>(dh), ptr<__bf16>(dht), (int)ldt, ptr<__bf16>(pool), ptr<__bf16>(wf1t),
                  (int)B, gwf1.data_ptr<float>(), ptr<__bf16>(dpool), head_slab.data_ptr<float>(),
                  (int)hb, gwf2.data_ptr<float>(), gbf2.data_ptr<float>(), gbf1.data_ptr<float>(),
-                 metrics.data_ptr<double>(), make_fc_update(fc_update), cur_stream(dh));
+                 metrics.data_ptr<double>(), fcu, cur_stream(dh));
 }
 
 static int64_t conv_blocks(int64_t B, int64_t ipb, int64_t bands) {
@@ -679,19 +692,20 @@ void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int
 }
 
 void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor pmask, at::Tensor w2,
-                  int64_t B, at::Tensor slab) {
+                  int64_t B, at::Tensor slab, int64_t ipb) {
   c10::DeviceGuard g(a1g.device());
-  TORCH_CHECK(B >= 1, "B must be >= 1");
+  TORCH_CHECK(B >= 1 && ipb >= 1, "B and ipb must be >= 1");
   need_min(a1g, at::kFloat, B * 676 * 32, "a1g");
   need_min(xng, at::kFloat, B * 784, "xng");
   need_min(dpool, at::kFloat, B * CNN_FEAT, "dpool");
   need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
   need(w2, at::kFloat, "w2");
   TORCH_CHECK(w2.numel() == 64 * 288, "conv2 weight");
-  need_min(slab, at::kFloat, (int64_t)f32_conv_bwd_blocks((int)B) * CNN_CONV_SLAB, "conv slab");
+  need_min(slab, at::kFloat, (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb) * CNN_CONV_SLAB,
+           "conv slab");
   launch_f32_conv_bwd(a1g.data_ptr<float>(), xng.data_ptr<float>(), dpool.data_ptr<float>(),
-                      pmask.data_ptr<uint8_t>(), w2.data_ptr<float>(), (int)B, slab.data_ptr<float>(),
-                      cur_stream(a1g));
+                      pmask.data_ptr<uint8_t>(), w2.data_ptr<float>(), (int)B, (int)ipb,
+                      slab.data_ptr<float>(), cur_stream(a1g));
 }
 
 // Upload an instantiated hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device
@@ -771,8 +785,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"));
   m.def("f32_fc1_fwd", &f32_fc1_fwd);
   m.def("f32_fc1_bwd", &f32_fc1_bwd);
-  m.def("f32_conv_bwd", &f32_conv_bwd);
-  m.def("f32_conv_bwd_nblk", [](int64_t B) { return (int64_t)f32_conv_bwd_blocks((int)B); });
+  m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),
+        py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1);
+  m.def("f32_conv_bwd_nblk", [](int64_t B, int64_t ipb) {
+    return (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb); }, py::arg("B"), py::arg("ipb") = 1);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);
   m.def("read_stamps", &read_stamps);
   m.def("graph_upload", &graph_upload);

@@ -113,7 +113,8 @@ void launch_optim(int kind, OptArgs& a, hipStream_t st);
 // World size 1: the fc1-weight update fused into fc1_bwd's weight-gradient tiles (the tile
 // is final in registers; nothing else in the step reads the fp32 weights or the bf16 [n][k]
 // copy until the next step's fc1_fwd -- the transposed copy that this step's dX tiles read
-// is re-derived later by the optimizer launch).  kind < 0: off; OPT_SGD only.  Same
+// is re-derived later by the optimizer launch, or double-buffered: shadow_t2).  kind < 0:
+// off; OPT_SGD only.  Same
 // hyper-parameter fields as OptArgs.
 struct FcUpdate {
   int kind;
@@ -123,6 +124,11 @@ struct FcUpdate {
   float* m;
   float* v;
   __bf16* shadow;       // bf16 copy, same layout
+  // optional: the transposed copy W1^T double-buffered (2 x numel, fragment-major): this
+  // launch's dX tiles read half (step & 1) and its weight tiles write the updated copy into
+  // half ((step + 1) & 1), which the next step reads -- the optimizer launch no longer
+  // re-derives W1^T
+  __bf16* shadow_t2;
   const double* lr;
   const int64_t* step;
   double beta1_d, beta2_d;
@@ -158,13 +164,14 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
                     int32_t* ylab, hipStream_t st);
 // small batches: each image over `bands` in {2, 3, 6} workgroups of 24 / bands conv2 rows
-// (cnn_fwd_band.hip); same pool / pmask / ylab as launch_cnn_fwd; training (a1g != null) also
-// writes the a1 image and the normalised x for cnn_bwd_band instead of the uint8 x
+// (cnn_fwd_band.hip); same pool / pmask / ylab as launch_cnn_fwd; training also writes the a1
+// image and the normalised x for cnn_bwd_band (a1g, xng) and / or the gathered uint8 image for
+// cnn_bwd (xg)
 void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                          int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
-                         __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, int32_t* ylab,
-                         hipStream_t st);
+                         __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, uint8_t* xg,
+                         int32_t* ylab, hipStream_t st);
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st);
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,
@@ -203,9 +210,11 @@ void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, 
 void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
                         float* gwf1, float* dpool, const float* head_slab, int head_blocks,
                         float* gwf2, float* gbf2, float* gbf1, double* metrics, hipStream_t st);
-int f32_conv_bwd_blocks(int B);
+// conv backward: (image group of ipb images, row band) workgroups, one slab each
+int f32_conv_bwd_blocks(int B, int ipb);
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
-                         const uint8_t* pmask, const float* w2, int B, float* slab, hipStream_t st);
+                         const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
+                         hipStream_t st);
 
 // diagnostic timestamps (all zero unless built with PDM_STAMPS=1)
 void read_stamps_fwd(unsigned long long* host);

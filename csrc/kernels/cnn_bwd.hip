@@ -68,8 +68,12 @@ constexpr int NXCD = 8;              // MI355X: workgroups are dealt round-robin
 static_assert(DX_TILES % NXCD == 0 && DW_TILES % NXCD == 0, "XCD-aware tile mapping");
 constexpr int HR_BLOCKS = (HEAD_SLAB + 63) / 64;   // head-slab reduction workgroups (23)
 
-__device__ __forceinline__ int tile_off(int row, int byte) {  // [32 rows][128 B], 2-way-free tr reads
-  return row * 128 + (byte ^ (((row >> 3) & 1) << 5));
+// [rows][128 B] pool tile.  A transposed read's 32-lane half touches rows {0-3, 8-11} (+4)
+// of a 16-row block at one 32-B column chunk each: rows of equal parity share banks, so the
+// chunk is XORed with row bits 1 and 3 -> the 8 chunks cover all 64 banks once
+// (tools/lds_bank_model.py; the bit-3-only swizzle was 2 passes per read)
+__device__ __forceinline__ int tile_off(int row, int byte) {
+  return row * 128 + (byte ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 5));
 }
 
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(
@@ -78,7 +82,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     bf16* __restrict__ dpool, const float* __restrict__ head_slab, int head_blocks,
     float* __restrict__ gwf2, float* __restrict__ gbf2, float* __restrict__ gbf1,
     double* __restrict__ metrics, int bid_offset, const FcUpdate fcu) {
-  __shared__ __attribute__((aligned(16))) char tile[DWC * 128];
+  // [0, 16 KB): the pool tile, then the fused update's bf16 W1 fragments; [16 KB, 32 KB):
+  // the fused update's W1^T fragments (double-buffered W1^T only)
+  __shared__ __attribute__((aligned(16))) char tile[2 * DWC * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
   const int nd = (ldt / 32) * DX_TILES;
@@ -183,21 +189,30 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       // is 8 n-tiles x 2 k-steps of 1-KB blocks, assembled in LDS and stored as 16-B chunks
       __syncthreads();   // every wave's last reads of the pool tile are done
       bf16* fr = reinterpret_cast<bf16*>(tile);
+      // W1^T fragments of this tile (kernels.h shadow_t_pos, m = feature): 4 n-tiles x 4
+      // 16-feature blocks of 1 KB, one contiguous 16 KB range; a lane's 4 rows r are 4
+      // consecutive bf16 (one 8-B store, 512 B contiguous per wave store)
+      bf16* frt = reinterpret_cast<bf16*>(tile + DWC * 128);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int nt = 0; nt < 4; ++nt) {
+          bf16 pt[4];
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
+          for (int r = 0; r < 4; ++r) {
             const int n = wave * 32 + mt * 16 + 4 * g + r, kl = 16 * nt + i16;
             const int64_t q = (int64_t)n * FEAT + k0 + kl;
             float m = fmv[mt][r][nt], v = 0.f;
             const float p = update<OPT_SGD>(fpv[mt][r][nt], acc[mt][nt][r], m, v, h, fcu.grad_scale);
             fcu.p[q] = p;
             fcu.m[q] = m;
-            fr[(((n >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (n & 15)) * 8 + (kl & 7)] =
-                to_bf16(p);
+            pt[r] = to_bf16(p);
+            fr[(((n >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (n & 15)) * 8 + (kl & 7)] = pt[r];
           }
+          if (fcu.shadow_t2 != nullptr)
+            *reinterpret_cast<bf16x4*>(frt + (((nt * 4 + wave) * 64 + (mt * 2 + (g >> 1)) * 16 + i16) * 8 +
+                                              (g & 1) * 4)) = bf16x4{pt[0], pt[1], pt[2], pt[3]};
+        }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -205,6 +220,12 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         *reinterpret_cast<uint4*>(fcu.shadow + ((int64_t)((blk >> 1) * (FEAT / 32) + (k0 >> 5) +
                                                           (blk & 1)) * 64 + (c & 63)) * 8) =
             reinterpret_cast<const uint4*>(fr)[c];
+      }
+      if (fcu.shadow_t2 != nullptr) {
+        bf16* wt_next = fcu.shadow_t2 + ((*fcu.step + 1) & 1) * ((int64_t)FEAT * HID) + (int64_t)k0 * HID;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          reinterpret_cast<uint4*>(wt_next)[tid + 256 * u] = reinterpret_cast<const uint4*>(frt)[tid + 256 * u];
       }
     }
     FC_STAMP(bid, 13);
@@ -224,6 +245,8 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     // of W1^T.
     const int t = bid - DW_TILES;
     FC_STAMP(t, 0);
+    // double-buffered W1^T (fused update): this step's copy is half (step & 1)
+    if (fcu.kind >= 0 && fcu.shadow_t2 != nullptr) wf1t += (*fcu.step & 1) * ((int64_t)FEAT * HID);
     constexpr int TPX = DX_TILES / NXCD;                 // feature tiles per XCD
     const int xcd = t % NXCD, loc = t / NXCD;
     const int b0 = (loc / TPX) * 32;

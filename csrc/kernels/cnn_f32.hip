@@ -110,39 +110,60 @@ __global__ __launch_bounds__(FT, 1) void f32_fwd_kernel(
     float bias[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) bias[nt] = ws[320 + nh * 32 + nt * 16 + i16];
-    for (int tt = wave; tt < 36; tt += 8) {
-      const int py = tt / 3, px0 = 4 * (tt - py * 3);
-      const int pb = (2 * py + (s >> 1)) * H1 + 2 * (px0 + q) + (s & 1);   // a1 pixel, tap 0
-      f32x4 acc[2];
+    // tiles {wave + 8 k} in pairs: four independent accumulator chains, every operand read of
+    // a tap (8 A values per tile, 16 B values shared by both tiles) issued before its MFMAs
+    for (int tt0 = wave; tt0 < 36; tt0 += 16) {
+      const bool two = tt0 + 8 < 36;
+      int pb[2];
+      f32x4 acc[2][2];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[nt] = f32x4{bias[nt], bias[nt], bias[nt], bias[nt]};
+      for (int u = 0; u < 2; ++u) {
+        const int tt = min(tt0 + 8 * u, 35);
+        const int py = tt / 3, px0 = 4 * (tt - py * 3);
+        pb[u] = (2 * py + (s >> 1)) * H1 + 2 * (px0 + q) + (s & 1);   // a1 pixel, tap 0
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[u][nt] = f32x4{bias[nt], bias[nt], bias[nt], bias[nt]};
+      }
 #pragma unroll 1
       for (int tap = 0; tap < 9; ++tap) {
-        const float* ap = a1 + (pb + (tap / 3) * H1 + tap % 3) * A1S + g;
+        const int toff = (tap / 3) * H1 + tap % 3;
+        float av[2][8], bv[2][8];
 #pragma unroll
         for (int c8 = 0; c8 < 8; ++c8) {
           const int k = tap * 32 + c8 * 4 + g;
-          const float av = ap[c8 * 4];
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
-            acc[nt] = mfma4(av, w2h[w2h_off(k, nt * 16 + i16)], acc[nt]);
+          for (int u = 0; u < 2; ++u) av[u][c8] = a1[(pb[u] + toff) * A1S + g + c8 * 4];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) bv[nt][c8] = w2h[w2h_off(k, nt * 16 + i16)];
         }
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[u][nt] = mfma4(av[u][c8], bv[nt][c8], acc[u][nt]);
       }
-      const int pp = py * HP + px0 + g;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int co = nh * 32 + nt * 16 + i16;
-        float m = acc[nt][0];
-        uint32_t oh = 1u;
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        const int tt = tt0 + 8 * u;
+        const int py = tt / 3, px0 = 4 * (tt - py * 3);
+        const int pp = py * HP + px0 + g;
 #pragma unroll
-        for (int r = 1; r < 4; ++r) {
-          const bool gt = acc[nt][r] > m;   // first position holding the max
-          m = gt ? acc[nt][r] : m;
-          oh = gt ? (1u << r) : oh;
+        for (int nt = 0; nt < 2; ++nt) {
+          const int co = nh * 32 + nt * 16 + i16;
+          float m = acc[u][nt][0];
+          uint32_t oh = 1u;
+#pragma unroll
+          for (int r = 1; r < 4; ++r) {
+            const bool gt = acc[u][nt][r] > m;   // first position holding the max
+            m = gt ? acc[u][nt][r] : m;
+            oh = gt ? (1u << r) : oh;
+          }
+          const bool pos = m > 0.f;
+          pool[(int64_t)img * FEAT + pp * C2 + co] = pos ? m : 0.f;
+          if (TRAIN) pmask[(int64_t)img * FEAT + pp * C2 + co] = (uint8_t)(pos ? 0x80u | oh : 0u);
         }
-        const bool pos = m > 0.f;
-        pool[(int64_t)img * FEAT + pp * C2 + co] = pos ? m : 0.f;
-        if (TRAIN) pmask[(int64_t)img * FEAT + pp * C2 + co] = (uint8_t)(pos ? 0x80u | oh : 0u);
       }
     }
   }
@@ -387,116 +408,152 @@ __device__ __forceinline__ int w2t_off(int tap, int co, int ci) {
 
 __global__ __launch_bounds__(FT, 1) void f32_conv_bwd_kernel(
     const float* __restrict__ a1g, const float* __restrict__ xng, const float* __restrict__ dpool,
-    const uint8_t* __restrict__ pmask, const float* __restrict__ w2, float* __restrict__ slab) {
+    const uint8_t* __restrict__ pmask, const float* __restrict__ w2, int B, int ipb,
+    float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) char smem[CB_TOTAL];
   float* xs = reinterpret_cast<float*>(smem + CB_XS);
   float* a1 = reinterpret_cast<float*>(smem + CB_A1);
   float* dz = reinterpret_cast<float*>(smem + CB_DZ);
   float* w2t = reinterpret_cast<float*>(smem + CB_W2);
-  const int img = blockIdx.x / CB_S, band = blockIdx.x - img * CB_S;
+  const int grp = blockIdx.x / CB_S, band = blockIdx.x - grp * CB_S;
   const int d0 = band * CB_R;
   const int aown = band == CB_S - 1 ? CB_R + 2 : CB_R;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   float* out = slab + (int64_t)blockIdx.x * CNN_CONV_SLAB;
-  // ---- staging: zero dz2, x / a1 rows, W2^T
-  for (int i = tid; i < (2 + CB_ZR * H1) * DZS / 4; i += FT)
-    reinterpret_cast<float4*>(dz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int i = tid; i < (CB_R + 4) * IMG; i += FT)
-    xs[i] = xng[(int64_t)img * 784 + d0 * IMG + i];
-  for (int i = tid; i < (CB_R + 2) * H1 * C1; i += FT) {
-    const int p = i >> 5, c = i & 31;
-    a1[p * A1S + c] = a1g[((int64_t)img * P1 + d0 * H1) * C1 + i];
-  }
+  const int pr0 = band == 0 ? 0 : d0 / 2 - 1;
+  const int npr = d0 / 2 + CB_R / 2 - pr0;
+  const int npx = aown * H1, nmt = (npx + 15) / 16;
+  // W2^T once per workgroup (its images share the band)
   for (int e = tid; e < C2 * 288; e += FT) {
     const int co = e / 288, k = e - co * 288;
     w2t[w2t_off(k >> 5, co, k & 31)] = w2[e];
   }
-  __syncthreads();
-  // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (halo row above included) + db2 of the
-  // band's own pooled rows; thread -> fixed channel co = tid & 63
-  const int pr0 = band == 0 ? 0 : d0 / 2 - 1;
-  const int npr = d0 / 2 + CB_R / 2 - pr0;
-  float db2p = 0.f;
-  for (int it = tid; it < npr * HP * C2; it += FT) {
-    const int pl = it >> 6, co = it & 63;
-    const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
-    const int gi = (py * HP + px) * C2 + co;
-    const uint8_t mk = pmask[(int64_t)img * FEAT + gi];
-    if (mk & 0x80) {
-      const float v = dpool[(int64_t)img * FEAT + gi];
-      const int sidx = __builtin_ctz((unsigned)mk & 0xf);
-      const int lr = 2 * py + (sidx >> 1) - (d0 - 2);   // local dz2 row
-      dz[(2 + lr * H1 + 2 * px + (sidx & 1)) * DZS + co] = v;
-      if (py >= d0 / 2) db2p += v;
-    }
-  }
-  __syncthreads();
-  // ---- conv2 dgrad over the band's own a1 pixels (m-tiles of 16 pixels p = 26 y + x, N = 32
-  // ci, K = 9 taps x 64 co) + relu'(a1) + conv1 weight/bias gradient on the fp32 MFMA:
-  // dW1[ci][tap] += sum_p dz1[p][ci] x[p + tap]; the dgrad accumulator (rows = pixels, cols = ci)
-  // already is its A operand (M = ci, K = pixel), the B operand is x (N = tap, 9 = bias ones)
+  // accumulators that persist over the workgroup's images: conv2 wgrad tiles t = wave + 8 j
+  // (72 = 4 co tiles x 18 (tap, ci tile)), the conv1 weight/bias partials, db2
+  f32x4 wacc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) wacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  const int npx = aown * H1, nmt = (npx + 15) / 16;
-  for (int mt = wave; mt < nmt; mt += 8) {
-    const int p = min(mt * 16 + i16, npx - 1);           // A row: this lane's pixel
-    const int y = p / H1, x = p - y * H1;
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float db2p = 0.f;
+  for (int ii = 0; ii < ipb; ++ii) {
+    const int img = grp * ipb + ii;
+    if (img >= B) break;                           // workgroup-uniform
+    __syncthreads();   // the previous image's reads of dz2 / a1 / x are done
+    // ---- staging: zero dz2, x / a1 rows
+    for (int i = tid; i < (2 + CB_ZR * H1) * DZS / 4; i += FT)
+      reinterpret_cast<float4*>(dz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < (CB_R + 4) * IMG; i += FT) xs[i] = xng[(int64_t)img * 784 + d0 * IMG + i];
+    for (int i = tid; i < (CB_R + 2) * H1 * C1; i += FT) {
+      const int p = i >> 5, c = i & 31;
+      a1[p * A1S + c] = a1g[((int64_t)img * P1 + d0 * H1) * C1 + i];
+    }
+    __syncthreads();
+    // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows);
+    // thread -> fixed channel co = tid & 63
+    for (int it = tid; it < npr * HP * C2; it += FT) {
+      const int pl = it >> 6, co = it & 63;
+      const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
+      const int gi = (py * HP + px) * C2 + co;
+      const uint8_t mk = pmask[(int64_t)img * FEAT + gi];
+      if (mk & 0x80) {
+        const float v = dpool[(int64_t)img * FEAT + gi];
+        const int sidx = __builtin_ctz((unsigned)mk & 0xf);
+        const int lr = 2 * py + (sidx >> 1) - (d0 - 2);
+        dz[(2 + lr * H1 + 2 * px + (sidx & 1)) * DZS + co] = v;
+        if (py >= d0 / 2) db2p += v;
+      }
+    }
+    __syncthreads();
+    // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias gradient
+    // (see the file comment); per tap every operand read is issued before its 32 MFMAs
+    for (int mt = wave; mt < nmt; mt += 8) {
+      const int p = min(mt * 16 + i16, npx - 1);
+      const int y = p / H1, x = p - y * H1;
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - 3 * ky;
-      const float* ap = dz + (2 + (y + 2 - ky) * H1 + x - kx) * DZS + g;
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const float* ap = dz + (2 + (y + 2 - ky) * H1 + x - kx) * DZS + g;
+        float av[16], bv[2][16];
 #pragma unroll
-      for (int c16 = 0; c16 < 16; ++c16) {
-        const float av = ap[c16 * 4];
-        const int co = c16 * 4 + g;
+        for (int c16 = 0; c16 < 16; ++c16) {
+          av[c16] = ap[c16 * 4];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma4(av, w2t[w2t_off(tap, co, nt * 16 + i16)], acc[nt]);
+          for (int nt = 0; nt < 2; ++nt) bv[nt][c16] = w2t[w2t_off(tap, c16 * 4 + g, nt * 16 + i16)];
+        }
+#pragma unroll
+        for (int c16 = 0; c16 < 16; ++c16)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma4(av[c16], bv[nt][c16], acc[nt]);
+      }
+      float xb[4];
+      const int ctap = i16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = mt * 16 + 4 * g + r;
+        const int yy = pr / H1, xx = pr - yy * H1;
+        const bool valid = pr < npx;
+        xb[r] = !valid ? 0.f
+                : ctap < 9 ? xs[(yy + ctap / 3) * IMG + xx + ctap % 3]
+                : ctap == 9 ? 1.f : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const float a1v = valid ? a1[min(pr, npx - 1) * A1S + nt * 16 + i16] : 0.f;
+          acc[nt][r] = (valid && a1v > 0.f) ? acc[nt][r] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
+    }
+    // ---- conv2 wgrad over the band's own dz2 rows into the persistent tile accumulators:
+    // two tiles per pass (independent accumulator chains), operands of 6 k-steps per batch
+#pragma unroll
+    for (int jp = 0; jp < 9; jp += 2) {
+      const int nj = jp + 1 < 9 ? 2 : 1;
+      int dzo[2], a1o[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 8 * min(jp + u, 8);
+        const int mt = t / 18, nn = t - mt * 18;
+        const int tap = nn >> 1, ct = nn & 1;
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        dzo[u] = (2 + 2 * H1 + g) * DZS + mt * 16 + i16;
+        a1o[u] = (ky * H1 + g + kx) * A1S + ct * 16 + i16;
+      }
+#pragma unroll
+      for (int ks0 = 0; ks0 < CB_R * 6; ks0 += 6) {
+        float av[2][6], bv[2][6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const int ks = ks0 + k, rr = ks / 6, c0 = (ks - rr * 6) * 4;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            av[u][k] = dz[dzo[u] + (rr * H1 + c0) * DZS];
+            bv[u][k] = a1[a1o[u] + (rr * H1 + c0) * A1S];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            if (u < nj) wacc[jp + u] = mfma4(av[u][k], bv[u][k], wacc[jp + u]);
       }
     }
-    // epilogue: lane holds da1 of pixels mt * 16 + 4 g + r, channel nt * 16 + i16
-    float xb[4];
-    const int ctap = i16;                                  // conv1-wgrad column: tap / bias
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int pr = mt * 16 + 4 * g + r;
-      const int yy = pr / H1, xx = pr - yy * H1;
-      const bool valid = pr < npx;
-      xb[r] = !valid ? 0.f
-              : ctap < 9 ? xs[(yy + ctap / 3) * IMG + xx + ctap % 3]
-              : ctap == 9 ? 1.f : 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const float a1v = valid ? a1[min(pr, npx - 1) * A1S + nt * 16 + i16] : 0.f;
-        acc[nt][r] = (valid && a1v > 0.f) ? acc[nt][r] : 0.f;   // dz1 = da1 relu'(a1)
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
-  }
-  // ---- conv2 wgrad over the band's own dz2 rows: tiles (co tile, tap x ci tile) = 4 x 18,
-  // K = 4 rows x 24 columns (k-steps of 4 pixels of one row)
-  for (int t = wave; t < 72; t += 8) {
-    const int mt = t / 18, nn = t - mt * 18;
-    const int tap = nn >> 1, ct = nn & 1;
-    const int ky = tap / 3, kx = tap - 3 * ky;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < CB_R * 6; ++ks) {
-      const int rr = ks / 6, c0 = (ks - rr * 6) * 4;
-      const float av = dz[(2 + (rr + 2) * H1 + c0 + g) * DZS + mt * 16 + i16];
-      const float bv = a1[((rr + ky) * H1 + c0 + g + kx) * A1S + ct * 16 + i16];
-      acc = mfma4(av, bv, acc);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16] = acc[r];
   }
   __syncthreads();   // dz2 region free: reduction scratch
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int t = wave + 8 * j;
+    const int mt = t / 18, nn = t - mt * 18;
+    const int tap = nn >> 1, ct = nn & 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16] = wacc[j][r];
+  }
   float* red = dz;
-  // conv1 partials acc1[nt]: rows ci = nt * 16 + 4 g + r, column tap = i16
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -543,9 +600,11 @@ void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float
                                            head_blocks, gwf2, gbf2, gbf1, metrics);
 }
 
-int f32_conv_bwd_blocks(int B) { return B * CB_S; }
+int f32_conv_bwd_blocks(int B, int ipb) { return ((B + ipb - 1) / ipb) * CB_S; }
 
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
-                         const uint8_t* pmask, const float* w2, int B, float* slab, hipStream_t st) {
-  f32_conv_bwd_kernel<<<B * CB_S, FT, 0, st>>>(a1g, xng, dpool, pmask, w2, slab);
+                         const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
+                         hipStream_t st) {
+  f32_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(a1g, xng, dpool, pmask, w2, B,
+                                                                   ipb, slab);
 }

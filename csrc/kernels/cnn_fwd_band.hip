@@ -47,7 +47,8 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
-    bf16* __restrict__ a1g, bf16* __restrict__ xng, int32_t* __restrict__ ylab) {
+    bf16* __restrict__ a1g, bf16* __restrict__ xng, uint8_t* __restrict__ xg,
+    int32_t* __restrict__ ylab) {
   using L = FwdBand<R>;
   constexpr int S = L::S;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
@@ -126,8 +127,12 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     // training: the band's own rows of the normalised bf16 image (the last band also rows
     // 24-27) for the backward's conv1 weight gradient
     const int own = band == S - 1 ? XW : R * 7;
-    if (TRAIN && tid < own)
-      reinterpret_cast<bf16x4*>(xng + (int64_t)img * 784)[d0 * 7 + tid] = bf16x4{v[0], v[1], v[2], v[3]};
+    if (TRAIN && tid < own) {
+      if (xng != nullptr)
+        reinterpret_cast<bf16x4*>(xng + (int64_t)img * 784)[d0 * 7 + tid] = bf16x4{v[0], v[1], v[2], v[3]};
+      // the one-image backward (cnn_bwd) reads the gathered uint8 image instead
+      if (xg != nullptr) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[d0 * 7 + tid] = xw;
+    }
   }
   __syncthreads();
   PDM_STAMP(2);
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
   if ((wave & 3) >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W2 DMA landed
   __syncthreads();
   PDM_STAMP(3);
-  if (TRAIN) {
+  if (TRAIN && a1g != nullptr) {
     // the band's own a1 rows (the last band also 24, 25), in the LDS image's swizzled layout,
     // for the backward (cnn_bwd_band copies them back by LDS-DMA instead of recomputing
     // conv1); a contiguous byte range of the image's [26][26][32] a1
@@ -243,14 +248,14 @@ template <int R>
 void launch_band(const uint8_t* images, const int32_t* labels, const int32_t* idx, int64_t nrow,
                  const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
                  const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, __bf16* a1g,
-                 __bf16* xng, int32_t* ylab, hipStream_t st) {
+                 __bf16* xng, uint8_t* xg, int32_t* ylab, hipStream_t st) {
   const int nblk = B * FwdBand<R>::S;
-  if (a1g != nullptr)
+  if (a1g != nullptr || xg != nullptr)
     cnn_fwd_band_kernel<R, true><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1,
-                                                       w2, b2, pool, pmask, a1g, xng, ylab);
+                                                       w2, b2, pool, pmask, a1g, xng, xg, ylab);
   else
     cnn_fwd_band_kernel<R, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1,
-                                                        b1, w2, b2, pool, pmask, a1g, xng, ylab);
+                                                        b1, w2, b2, pool, pmask, a1g, xng, xg, ylab);
 }
 
 }  // namespace
@@ -258,20 +263,20 @@ void launch_band(const uint8_t* images, const int32_t* labels, const int32_t* id
 void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                          int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
-                         __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, int32_t* ylab,
-                         hipStream_t st) {
+                         __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, uint8_t* xg,
+                         int32_t* ylab, hipStream_t st) {
   switch (bands) {
     case 2:
       launch_band<12>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
-                      ylab, st);
+                      xg, ylab, st);
       break;
     case 3:
       launch_band<8>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
-                     ylab, st);
+                     xg, ylab, st);
       break;
     case 6:
       launch_band<4>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
-                     ylab, st);
+                     xg, ylab, st);
       break;
     default:
       break;   // bind.cpp validates bands

@@ -15,12 +15,24 @@ program (``cnn_step.py``), on the fp32 matrix cores (``csrc/kernels/cnn_f32.hip`
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .gpu_step import GpuStepBase
 
 EVAL_CHUNK = 2048
 SPLITK_TRAIN = 32        # fc1 split-K (divides 288: whole 32-float k chunks per split)
+
+
+def conv_ipb(B: int) -> int:
+    """Images per fp32 conv-backward workgroup (each workgroup stages W2^T once and writes one
+    slab for its images' row band): PDM_F32_IPB overrides."""
+    env = os.environ.get("PDM_F32_IPB")
+    if env:
+        return max(1, int(env))
+    # B = 256, 100-step bench: ipb 1 / 2 / 3 / 6 = 360 / 351 / 340 / 416 us per step
+    return max(1, -(-B * 6 // 512))          # <= 2 rounds of 256 workgroups
 
 
 def splitk_eval(b: int) -> int:
@@ -52,8 +64,9 @@ class CnnStepF32(GpuStepBase):
         self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=f32,
                                      device=dev)
         self.dpool = torch.empty(B * 9216, dtype=f32, device=dev)
-        self.conv_slab = torch.empty(C.f32_conv_bwd_nblk(B) * C.CNN_CONV_SLAB, dtype=f32,
-                                     device=dev)
+        self.conv_slab = torch.empty(max(C.f32_conv_bwd_nblk(b, conv_ipb(b))
+                                         for b in range(1, B + 1)) * C.CNN_CONV_SLAB,
+                                     dtype=f32, device=dev)
         a = self.arena
         self.P = {n: a.param(n) for n in ("conv1.weight", "conv1.bias", "conv2.weight",
                                           "conv2.bias", "fc1.weight", "fc1.bias", "fc2.weight",
@@ -122,9 +135,10 @@ class CnnStepF32(GpuStepBase):
                       self.metrics.train_view())
         red = self.reducer
         red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
+        ipb = conv_ipb(B)
         C.f32_conv_bwd(self.a1g, self.xng, self.dpool, self.pmask, P["conv2.weight"], B,
-                       self.conv_slab)
-        nblk = C.f32_conv_bwd_nblk(B)
+                       self.conv_slab, ipb)
+        nblk = C.f32_conv_bwd_nblk(B, ipb)
         if self.fuse_conv_reduce:
             self.launch_optimizer(self._fused_segments(nblk))
             return

@@ -91,6 +91,16 @@ def choose_bands(B: int, cus: int = 256) -> int:
     return 1
 
 
+def choose_fwd_bands(B: int) -> int:
+    """Row bands per image in the forward: the backward's split (the band backward reads the
+    band forward's a1 / normalised x); PDM_FWD_BANDS forces a split of the forward alone (it
+    then hands the one-image backward the uint8 image, as cnn_fwd does)."""
+    forced = os.environ.get("PDM_FWD_BANDS")
+    if forced is not None and choose_bands(B) == 1:
+        return int(forced)
+    return choose_bands(B)
+
+
 def conv_blocks(C, B: int) -> int:
     """Conv-backward workgroups (= gradient slabs) for per-rank batch B."""
     bands = choose_bands(B)
@@ -133,7 +143,9 @@ class CnnStep(GpuStepBase):
                                      device=dev)
         # bf16 compute copies of the weights (kept current by the optimizer kernel)
         self.wf1 = torch.empty(128 * 9216, dtype=bf16, device=dev)
-        self.wf1t = torch.empty(9216 * 128, dtype=bf16, device=dev)
+        # W1^T: two copies (double buffer of the fused world-size-1 fc1 update, see below);
+        # every other path reads and writes the first
+        self.wf1t = torch.empty(2 * 9216 * 128, dtype=bf16, device=dev)
         self.w2 = torch.empty(64 * 288, dtype=bf16, device=dev)
         self.w2t = torch.empty(288 * 64, dtype=bf16, device=dev)
         # parameter / gradient views (kernel layouts)
@@ -152,6 +164,10 @@ class CnnStep(GpuStepBase):
         # bf16 copy W1^T from the updated W1 (PDM_FUSE_FC1=0 disables)
         self.fuse_fc1 = (self.fuse_conv_reduce and self.opt.kind == "sgd" and
                          os.environ.get("PDM_FUSE_FC1", "1") != "0")
+        # ... and writes W1^T too, double-buffered by step parity (this step's dX tiles read
+        # one half while its weight tiles write the other), so the optimizer launch skips fc1
+        # entirely (PDM_FC1_WT2=0: the optimizer re-derives W1^T instead)
+        self.wt_double = os.environ.get("PDM_FC1_WT2", "1") != "0"
         self._fused = {}
         # RCCL data plane: defer the fc-bucket update past the next step's cnn_fwd so the
         # 4.7 MB all-reduce overlaps it (True), or reduce both buckets in one grouped RCCL
@@ -179,7 +195,10 @@ class CnnStep(GpuStepBase):
         """Re-derive the bf16 weight copies from the fp32 master weights."""
         w1 = self.arena.param("fc1.weight").reshape(128, 9216)
         self.wf1.copy_(frag_major(w1.to(torch.bfloat16)))
-        self.wf1t.copy_(frag_major_t(w1.to(torch.bfloat16)))
+        wt = frag_major_t(w1.to(torch.bfloat16))
+        n = wt.numel()
+        self.wf1t[:n].copy_(wt)
+        self.wf1t[n:].copy_(wt)
         w2 = self.arena.param("conv2.weight").reshape(64, 288)
         self.w2.copy_(frag_major(w2.to(torch.bfloat16)))
         self.w2t.copy_(w2.t().contiguous().reshape(-1).to(torch.bfloat16))
@@ -192,7 +211,8 @@ class CnnStep(GpuStepBase):
             if p.name == "fc1.weight":
                 # W1 and W1^T in the MFMA-fragment-major layout fc1_fwd / fc1_bwd's dX tiles
                 # read (kernels.h frag_pos)
-                segs.append((off, 128, 9216, self.wf1, self.wf1t, None, False, True, True))
+                segs.append((off, 128, 9216, self.wf1, self.wf1t[:128 * 9216], None, False, True,
+                             True))
             elif p.name == "conv2.weight":
                 # W2 fragment-major (cnn_fwd's conv2 B operand), W2^T row-major (cnn_bwd's
                 # LDS image)
@@ -232,8 +252,10 @@ class CnnStep(GpuStepBase):
             for sg in self._opt_segments:
                 name = by_off.get(sg[0])
                 if name is None and self.fuse_fc1 and sg[0] == fc1_off:
-                    # updated by fc1_bwd: only W1^T = transpose(W1) is left to write
-                    plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True, True, True))
+                    # updated by fc1_bwd: only W1^T = transpose(W1) is left to write, unless
+                    # fc1_bwd writes it too (double-buffered)
+                    if not self.wt_double:
+                        plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True, True, True))
                 elif name is None:
                     plain.append(sg)
                 else:
@@ -245,6 +267,14 @@ class CnnStep(GpuStepBase):
             segs = slab_segs + plain
             self._fused[nblk] = segs
         return segs
+
+    def fwd_outputs(self, B: int):
+        """cnn_fwd's training outputs for per-rank batch B: (xg, ylab, bands, a1g, xng) -- the
+        band backward reads a1 + normalised x, the one-image backward the uint8 image."""
+        fb = choose_fwd_bands(B)
+        if choose_bands(B) > 1:
+            return None, self.ylab, fb, self.a1g, self.xng
+        return self.xg, self.ylab, fb, None, None
 
     def _train_seq(self, B: int, n: int) -> None:
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
@@ -275,7 +305,7 @@ class CnnStep(GpuStepBase):
         bands = choose_bands(B)
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                  self.pmask, self.xg, self.ylab, bands, self.a1g, self.xng)
+                  self.pmask, *self.fwd_outputs(B))
         if carry_in:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(self._bucket_segments()[0])
@@ -357,7 +387,16 @@ class CnnStep(GpuStepBase):
         return (self.C.OPT_SGD, self.arena.params[off:off + n], self.reducer.out_grads[off:off + n],
                 o.momentum_buffer[off:off + n], None, self.wf1, o._lr_dev, o._step_dev, 0.0, 0.0,
                 0.0, float(g["weight_decay"]), float(g["momentum"]), float(g["dampening"]),
-                bool(g["nesterov"]), float(self.reducer.grad_scale))
+                bool(g["nesterov"]), float(self.reducer.grad_scale),
+                self.wf1t if self.wt_double else None)
+
+    def current_wf1t(self) -> torch.Tensor:
+        """The W1^T copy the next fc1_bwd reads (double buffer: half (next step & 1))."""
+        n = 128 * 9216
+        if self.fuse_fc1 and self.fuse_conv_reduce and self.wt_double:
+            h = (int(self.opt._step_dev.item()) + 1) & 1
+            return self.wf1t[h * n:(h + 1) * n]
+        return self.wf1t[:n]
 
     def evaluate(self) -> None:
         C, P = self.C, self.P

@@ -75,6 +75,30 @@ def test_cnn_forward_band_split(gpu, B, bands):
     assert (got != ref).float().mean().item() < 0.01      # bf16 rounding ties only
 
 
+@pytest.mark.parametrize("B,bands", [(64, 6), (37, 2)])
+def test_cnn_forward_band_split_uint8_handoff(gpu, B, bands):
+    """A forward-only band split (PDM_FWD_BANDS: the one-image backward stays) hands the
+    backward the gathered uint8 image, like cnn_fwd, with the same pool / mask / labels."""
+    prog, train, _ = _program(B)
+    st = prog.gpu
+    idx = distributed_indices(len(train), 1, 0, 0)
+    prog.set_train_indices(idx)
+    C, P = st.C, st.P
+    outs = []
+    for b in (1, bands):
+        for t in (st.pool, st.pmask, st.xg):
+            t.view(torch.uint8).fill_(0x55)
+        C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, st.ctr[0:1], st.bfull, B,
+                  P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"], st.pool, st.pmask,
+                  st.xg, st.ylab, b, None, None)
+        torch.cuda.synchronize()
+        outs.append([st.pool[:B * 9216].view(torch.uint8).clone(), st.pmask[:B * 9216].clone(),
+                     st.ylab[:B].clone(), st.xg[:B * 784].clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[1][3].view(B, 784).cpu(), train.images[idx[:B]])
+
+
 @pytest.mark.parametrize("B", [64, 37])
 def test_cnn_forward_kernels(gpu, B):
     prog, train, _ = _program(B)
@@ -210,21 +234,24 @@ def test_cnn_large_batch_steps(gpu):
 
 def test_fused_conv_reduce_matches_separate_pass(gpu):
     """world_size 1 folds the conv slab reduction into the optimizer launch and (SGD) the
-    fc1-weight update into cnn_bwd; every combination must give the same bits as
+    fc1-weight update into fc1_bwd (W1^T re-derived by the optimizer, or double-buffered and
+    written by fc1_bwd); every combination must give the same bits as
     conv_reduce + optimizer (same fixed summation order, same update op order), incl. a
     tail step and the bf16 weight copies the next step reads."""
     res = []
-    for fuse, fuse_fc1 in ((True, True), (True, False), (False, False)):
+    for fuse, fuse_fc1, wt2 in ((True, True, True), (True, True, False), (True, False, False),
+                                (False, False, False)):
         prog, train, _ = _program(96, lr=0.05, n=96 * 3 + 40, seed=5)
         prog.gpu.fuse_conv_reduce = fuse
         prog.gpu.fuse_fc1 = fuse_fc1
+        prog.gpu.wt_double = wt2
         prog.gpu.invalidate_graphs()
         prog.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         prog.train_epoch()
         torch.cuda.synchronize()
         res.append((prog.arena.params.clone(), prog.arena.grads.clone(),
                     prog.optimizer.momentum_buffer.clone(), prog.gpu.wf1.clone(),
-                    prog.gpu.wf1t.clone()))
+                    prog.gpu.current_wf1t().clone()))
     for other in res[1:]:
         for a, b in zip(res[0], other):
             assert torch.equal(a, b)

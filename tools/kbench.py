@@ -55,7 +55,7 @@ def main():
       ks = {
           "cnn_fwd": lambda: C.cnn_fwd(st.ep_images.view(-1, 784), st.ep_labels, None, z, B, B,
                                        P["conv1.weight"], P["conv1.bias"], st.w2, P["conv2.bias"],
-                                       st.pool, st.pmask, st.xg, st.ylab, bands, st.a1g, st.xng),
+                                       st.pool, st.pmask, *st.fwd_outputs(B)),
           "fc1_fwd": lambda: C.fc1_fwd(st.pool, st.wf1, st.part, B, S),
           "cnn_head": lambda: C.cnn_head(st.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                                          st.ylab, True, st.dh, st.dht, ldt, st.head_slab,
