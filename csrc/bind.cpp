@@ -473,9 +473,9 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
 }
 
 // fc_update (world size 1, optional): (kind, p, g, m, v or None, shadow, lr, step, beta1,
-// beta2, eps, wd, momentum, dampening, nesterov, grad_scale[, shadow_t2]) -- the fc1-weight
-// update of the optimizer, run by fc1_bwd (kernels.h FcUpdate); shadow_t2 (2 x W1^T, the
-// tensor passed as wf1t) double-buffers the transposed copy
+// beta2, eps, wd, momentum, dampening, nesterov, grad_scale[, shadow_t_next]) -- the
+// fc1-weight update of the optimizer, run by fc1_bwd (kernels.h FcUpdate); shadow_t_next
+// receives the updated W1^T (the other half of the double buffer wf1t is read from)
 static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   FcUpdate u{};
   u.kind = -1;
@@ -514,13 +514,13 @@ static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   u.dampening = (float)a[13].cast<double>();
   u.nesterov = a[14].cast<bool>() ? 1 : 0;
   u.grad_scale = (float)a[15].cast<double>();
-  u.shadow_t2 = nullptr;
+  u.shadow_t_next = nullptr;
   if (a.size() == 17 && !a[16].is_none()) {
     auto t2 = a[16].cast<at::Tensor>();
-    need(t2, at::kBFloat16, "fc shadow_t2");
-    TORCH_CHECK(t2.numel() == 2 * u.numel, "fc_update: shadow_t2 holds two W1^T copies");
-    need_aligned(t2.data_ptr(), 16, "fc_update shadow_t2");
-    u.shadow_t2 = ptr<__bf16>(t2);
+    need(t2, at::kBFloat16, "fc shadow_t_next");
+    TORCH_CHECK(t2.numel() == u.numel, "fc_update: shadow_t_next is one W1^T copy");
+    need_aligned(t2.data_ptr(), 16, "fc_update shadow_t_next");
+    u.shadow_t_next = ptr<__bf16>(t2);
   }
   return u;
 }
@@ -547,8 +547,12 @@ void fc1_bwd(at::Tensor dh, at::Tensor dht, int64_t ldt, at::Tensor pool, at::Te
   need(metrics, at::kDouble, "metrics");
   need_numel(metrics, 3, "metrics");
   const FcUpdate fcu = make_fc_update(fc_update);
-  TORCH_CHECK(fcu.shadow_t2 == nullptr || fcu.shadow_t2 == ptr<__bf16>(wf1t),
-              "fc_update: shadow_t2 must be the wf1t double buffer");
+  if (fcu.shadow_t_next != nullptr) {
+    const char* r0 = reinterpret_cast<const char*>(wf1t.data_ptr());
+    const char* w0 = reinterpret_cast<const char*>(fcu.shadow_t_next);
+    const int64_t nb = (int64_t)CNN_FEAT * CNN_HID * 2;
+    TORCH_CHECK(w0 + nb <= r0 || r0 + nb <= w0, "fc_update: shadow_t_next overlaps the W1^T being read");
+  }
   launch_fc1_bwd(ptr<__bf16>(dh), ptr<__bf16>(dht), (int)ldt, ptr<__bf16>(pool), ptr<__bf16>(wf1t),
                  (int)B, gwf1.data_ptr<float>(), ptr<__bf16>(dpool), head_slab.data_ptr<float>(),
                  (int)hb, gwf2.data_ptr<float>(), gbf2.data_ptr<float>(), gbf1.data_ptr<float>(),

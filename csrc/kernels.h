@@ -113,7 +113,7 @@ void launch_optim(int kind, OptArgs& a, hipStream_t st);
 // World size 1: the fc1-weight update fused into fc1_bwd's weight-gradient tiles (the tile
 // is final in registers; nothing else in the step reads the fp32 weights or the bf16 [n][k]
 // copy until the next step's fc1_fwd -- the transposed copy that this step's dX tiles read
-// is re-derived later by the optimizer launch, or double-buffered: shadow_t2).  kind < 0:
+// is re-derived later by the optimizer launch, or double-buffered: shadow_t_next).  kind < 0:
 // off; OPT_SGD only.  Same
 // hyper-parameter fields as OptArgs.
 struct FcUpdate {
@@ -124,11 +124,10 @@ struct FcUpdate {
   float* m;
   float* v;
   __bf16* shadow;       // bf16 copy, same layout
-  // optional: the transposed copy W1^T double-buffered (2 x numel, fragment-major): this
-  // launch's dX tiles read half (step & 1) and its weight tiles write the updated copy into
-  // half ((step + 1) & 1), which the next step reads -- the optimizer launch no longer
-  // re-derives W1^T
-  __bf16* shadow_t2;
+  // optional: where the weight tiles write the updated W1^T copy (fragment-major) -- the
+  // other half of a double buffer whose current half this launch's dX tiles are reading
+  // (the host alternates the halves), so the optimizer launch no longer re-derives W1^T
+  __bf16* shadow_t_next;
   const double* lr;
   const int64_t* step;
   double beta1_d, beta2_d;

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
             pt[r] = to_bf16(p);
             fr[(((n >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (n & 15)) * 8 + (kl & 7)] = pt[r];
           }
-          if (fcu.shadow_t2 != nullptr)
+          if (fcu.shadow_t_next != nullptr)
             *reinterpret_cast<bf16x4*>(frt + (((nt * 4 + wave) * 64 + (mt * 2 + (g >> 1)) * 16 + i16) * 8 +
                                               (g & 1) * 4)) = bf16x4{pt[0], pt[1], pt[2], pt[3]};
         }
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
                                                           (blk & 1)) * 64 + (c & 63)) * 8) =
             reinterpret_cast<const uint4*>(fr)[c];
       }
-      if (fcu.shadow_t2 != nullptr) {
-        bf16* wt_next = fcu.shadow_t2 + ((*fcu.step + 1) & 1) * ((int64_t)FEAT * HID) + (int64_t)k0 * HID;
+      if (fcu.shadow_t_next != nullptr) {
+        bf16* wt_next = fcu.shadow_t_next + (int64_t)k0 * HID;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           reinterpret_cast<uint4*>(wt_next)[tid + 256 * u] = reinterpret_cast<const uint4*>(frt)[tid + 256 * u];
@@ -245,8 +245,6 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     // of W1^T.
     const int t = bid - DW_TILES;
     FC_STAMP(t, 0);
-    // double-buffered W1^T (fused update): this step's copy is half (step & 1)
-    if (fcu.kind >= 0 && fcu.shadow_t2 != nullptr) wf1t += (*fcu.step & 1) * ((int64_t)FEAT * HID);
     constexpr int TPX = DX_TILES / NXCD;                 // feature tiles per XCD
     const int xcd = t % NXCD, loc = t / NXCD;
     const int b0 = (loc / TPX) * 32;

@@ -285,7 +285,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #if PDM_WANT_FC1_FWD
 // ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
 constexpr int FC1_KB = 9;   // k-steps per load batch (288 k-steps = 32 batches)
-constexpr int FC1_AROW = FC1_KB * 32 * 2 + 16;   // LDS bytes per staged pool row (padded)
+constexpr int FC1_AROW = FC1_KB * 32 * 2 + 32;   // LDS bytes per staged pool row (padded)
 
 __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
@@ -311,8 +311,10 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
   const int n0 = wave * 32;
   // The pool tile (32 rows x 288 k per batch) is staged once per workgroup through LDS by
   // whole-line loads (it was read by each of the 4 waves, as 16 half lines per load);
-  // rows are padded to 592 B, so the A-fragment reads (16 rows x 16 B per lane group) are
-  // bank-conflict-free.  Rows past B read row B-1 (valid data, outputs never stored).
+  // rows are padded to 608 B, so the A-fragment reads (16 rows x 16 B per lane group) are
+  // bank-conflict-free (tools/lds_bank_model.py gfx950 ds_read_b128 lane groups: 592 B rows
+  // were 2 passes per read, 40 % conflict cycles in the PMC table).  Rows past B read row
+  // B-1 (valid data, outputs never stored).
   __shared__ __attribute__((aligned(16))) char at[32 * FC1_AROW];
   // W1 is fragment-major (kernels.h frag_pos): the 16 x 32 fragment (n-tile, k-step) is
   // one 1-KB block and this lane's 16 B sit at lane * 8 in it

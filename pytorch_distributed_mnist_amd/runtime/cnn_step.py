@@ -143,9 +143,11 @@ class CnnStep(GpuStepBase):
                                      device=dev)
         # bf16 compute copies of the weights (kept current by the optimizer kernel)
         self.wf1 = torch.empty(128 * 9216, dtype=bf16, device=dev)
-        # W1^T: two copies (double buffer of the fused world-size-1 fc1 update, see below);
-        # every other path reads and writes the first
-        self.wf1t = torch.empty(2 * 9216 * 128, dtype=bf16, device=dev)
+        # W1^T: two copies (double buffer of the fused world-size-1 fc1 update, see below:
+        # the step of phase p reads copy p and writes copy 1 - p); every other path reads and
+        # writes the first
+        self.wf1t2 = torch.empty(2, 9216 * 128, dtype=bf16, device=dev)
+        self.wf1t = self.wf1t2[0]
         self.w2 = torch.empty(64 * 288, dtype=bf16, device=dev)
         self.w2t = torch.empty(288 * 64, dtype=bf16, device=dev)
         # parameter / gradient views (kernel layouts)
@@ -168,6 +170,7 @@ class CnnStep(GpuStepBase):
         # one half while its weight tiles write the other), so the optimizer launch skips fc1
         # entirely (PDM_FC1_WT2=0: the optimizer re-derives W1^T instead)
         self.wt_double = os.environ.get("PDM_FC1_WT2", "1") != "0"
+        self.phase_period = 2 if self._wt_double_on() else 1
         self._fused = {}
         # RCCL data plane: defer the fc-bucket update past the next step's cnn_fwd so the
         # 4.7 MB all-reduce overlaps it (True), or reduce both buckets in one grouped RCCL
@@ -196,9 +199,8 @@ class CnnStep(GpuStepBase):
         w1 = self.arena.param("fc1.weight").reshape(128, 9216)
         self.wf1.copy_(frag_major(w1.to(torch.bfloat16)))
         wt = frag_major_t(w1.to(torch.bfloat16))
-        n = wt.numel()
-        self.wf1t[:n].copy_(wt)
-        self.wf1t[n:].copy_(wt)
+        self.wf1t2[0].copy_(wt)
+        self.wf1t2[1].copy_(wt)
         w2 = self.arena.param("conv2.weight").reshape(64, 288)
         self.w2.copy_(frag_major(w2.to(torch.bfloat16)))
         self.w2t.copy_(w2.t().contiguous().reshape(-1).to(torch.bfloat16))
@@ -211,8 +213,7 @@ class CnnStep(GpuStepBase):
             if p.name == "fc1.weight":
                 # W1 and W1^T in the MFMA-fragment-major layout fc1_fwd / fc1_bwd's dX tiles
                 # read (kernels.h frag_pos)
-                segs.append((off, 128, 9216, self.wf1, self.wf1t[:128 * 9216], None, False, True,
-                             True))
+                segs.append((off, 128, 9216, self.wf1, self.wf1t, None, False, True, True))
             elif p.name == "conv2.weight":
                 # W2 fragment-major (cnn_fwd's conv2 B operand), W2^T row-major (cnn_bwd's
                 # LDS image)
@@ -231,11 +232,6 @@ class CnnStep(GpuStepBase):
             b1 = [sg for sg in self._opt_segments if not (s0 <= sg[0] < e0)]
             self._bsegs = (b0, b1)
         return self._bsegs
-
-    def invalidate_graphs(self) -> None:
-        super().invalidate_graphs()
-        self._bsegs = None
-        self._fused = {}
 
     def _fused_segments(self, nblk: int):
         """Optimizer segments whose conv gradients are summed from `nblk` cnn_bwd slabs."""
@@ -287,6 +283,7 @@ class CnnStep(GpuStepBase):
             self.reducer.begin(n)        # one persistent xgmi collective for the n steps
         for i in range(n):
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
+            self.phase = (self.phase + 1) % self.phase_period
         if streamed:
             self.reducer.end()
 
@@ -313,7 +310,7 @@ class CnnStep(GpuStepBase):
         C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab, True,
                    self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
                    self.ctr[0:1], self.opt._step_dev, xs)
-        C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.wf1t, B, G["fc1.weight"], self.dpool,
+        C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.current_wf1t(), B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view(),
                   self._fc_update() if self.fuse_fc1 and self.fuse_conv_reduce else None)
@@ -388,15 +385,21 @@ class CnnStep(GpuStepBase):
                 o.momentum_buffer[off:off + n], None, self.wf1, o._lr_dev, o._step_dev, 0.0, 0.0,
                 0.0, float(g["weight_decay"]), float(g["momentum"]), float(g["dampening"]),
                 bool(g["nesterov"]), float(self.reducer.grad_scale),
-                self.wf1t if self.wt_double else None)
+                self.wf1t2[1 - self.phase] if self._wt_double_on() else None)
+
+    def _wt_double_on(self) -> bool:
+        return self.fuse_fc1 and self.fuse_conv_reduce and self.wt_double
 
     def current_wf1t(self) -> torch.Tensor:
-        """The W1^T copy the next fc1_bwd reads (double buffer: half (next step & 1))."""
-        n = 128 * 9216
-        if self.fuse_fc1 and self.fuse_conv_reduce and self.wt_double:
-            h = (int(self.opt._step_dev.item()) + 1) & 1
-            return self.wf1t[h * n:(h + 1) * n]
-        return self.wf1t[:n]
+        """The W1^T copy the next fc1_bwd reads."""
+        return self.wf1t2[self.phase] if self._wt_double_on() else self.wf1t
+
+    def invalidate_graphs(self) -> None:
+        super().invalidate_graphs()
+        self._bsegs = None
+        self._fused = {}
+        self.phase_period = 2 if self._wt_double_on() else 1
+        self.phase %= self.phase_period
 
     def evaluate(self) -> None:
         C, P = self.C, self.P

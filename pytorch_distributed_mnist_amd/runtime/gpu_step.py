@@ -61,6 +61,11 @@ class GpuStepBase:
         self.bfull = prog.batch_size
         self.metrics = prog.metrics
         self._opt_segments = None
+        # step phase for double-buffered operands (CnnStep's W1^T): a step reads the buffers of
+        # phase p and leaves the next step phase (p + 1) % phase_period.  A graph bakes in the
+        # phase it was captured at, so graphs are keyed by it as well.
+        self.phase = 0
+        self.phase_period = 1
 
     # -- data ----------------------------------------------------------------
     def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
@@ -102,15 +107,25 @@ class GpuStepBase:
     GRAPH_STEPS = 8
     GRAPH_SIZES = (8, 4, 2, 1)
 
-    def _graph(self, B: int, nsteps: int):
-        key = (B, nsteps)
+    def _graph(self, B: int, nsteps: int, phase=None):
+        phase = self.phase if phase is None else phase
+        key = (B, nsteps, phase)
         g = self.graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):          # captured on a side stream
-                self._train_seq(B, nsteps)
+            saved = self.phase
+            self.phase = phase
+            try:
+                with torch.cuda.graph(g):          # captured on a side stream
+                    self._train_seq(B, nsteps)
+            finally:
+                self.phase = saved              # capturing runs nothing
             self.graphs[key] = g
         return g
+
+    def _replay(self, B: int, nsteps: int) -> None:
+        self._graph(B, nsteps).replay()
+        self.phase = (self.phase + nsteps) % self.phase_period
 
     def prepare(self, B: int) -> None:
         """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES), so no
@@ -118,8 +133,8 @@ class GpuStepBase:
         when replayed."""
         if not self.use_graphs:
             return
-        for n in self.GRAPH_SIZES:
-            g = self._graph(B, n)
+        for n, ph in ((n, ph) for n in self.GRAPH_SIZES for ph in range(self.phase_period)):
+            g = self._graph(B, n, ph)
             try:
                 exe = g.raw_cuda_graph_exec()
             except (AttributeError, RuntimeError):
@@ -135,14 +150,12 @@ class GpuStepBase:
             return
         if self.use_graphs:
             k = self.GRAPH_STEPS
-            if n >= k:
-                gk = self._graph(B, k)
-                for _ in range(n // k):
-                    gk.replay()
+            for _ in range(n // k):
+                self._replay(B, k)
             r = n % k
             for size in self.GRAPH_SIZES[1:]:
                 if r & size:
-                    self._graph(B, size).replay()
+                    self._replay(B, size)
         else:
             self._train_seq(B, n)
         self.opt.step_count += n
@@ -157,6 +170,7 @@ class GpuStepBase:
             self.reducer.begin(n)        # one persistent collective launch for the n steps
         for _ in range(n):
             self._train_impl(B)
+            self.phase = (self.phase + 1) % self.phase_period
         if streamed:
             self.reducer.end()
 

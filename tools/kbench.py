@@ -60,7 +60,7 @@ def main():
           "cnn_head": lambda: C.cnn_head(st.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                                          st.ylab, True, st.dh, st.dht, ldt, st.head_slab,
                                          st.metrics.train_view(), None, None),
-          "fc1_bwd": lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"],
+          "fc1_bwd": lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.current_wf1t(), B, G["fc1.weight"],
                                        st.dpool, st.head_slab, G["fc2.weight"], G["fc2.bias"],
                                        G["fc1.bias"], st.metrics.train_view(),
                                        st._fc_update() if st.fuse_fc1 else None),

@@ -22,7 +22,7 @@ ldt = -(-B // 32) * 32
 st.train_step(B)
 torch.cuda.synchronize()
 role = os.environ.get("PDM_FC1BWD_ROLE", "all")
-us = timeit(lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"], st.dpool,
+us = timeit(lambda: C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.current_wf1t(), B, G["fc1.weight"], st.dpool,
                               st.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                               st.metrics.train_view(),
                               st._fc_update() if st.fuse_fc1 else None))

@@ -23,7 +23,7 @@ torch.cuda.synchronize()
 C, G = st.C, st.G
 ldt = -(-B // 32) * 32
 for _ in range(3):   # fc1_bwd alone (cnn_bwd would overwrite the stamps)
-    C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.wf1t, B, G["fc1.weight"], st.dpool, st.head_slab,
+    C.fc1_bwd(st.dh, st.dht, ldt, st.pool, st.current_wf1t(), B, G["fc1.weight"], st.dpool, st.head_slab,
               G["fc2.weight"], G["fc2.bias"], G["fc1.bias"], st.metrics.train_view(),
               st._fc_update() if st.fuse_fc1 else None)
 torch.cuda.synchronize()
