@@ -178,22 +178,27 @@ def main():
             torch.cuda.synchronize()
             return allmax(time.perf_counter() - t0)
 
-        def use(red, carry=True):
+        def use(red, carry="carry"):
             prog.reducer = red
             prog.gpu.reducer = red
             prog.gpu.use_graphs = bool(a.graphs) and red.capturable
             if hasattr(prog.gpu, "fc_carry"):
-                prog.gpu.fc_carry = carry
+                prog.gpu.fc_carry = carry != "nocarry"
+                prog.gpu.fc_side = carry == "side"
             prog.gpu.invalidate_graphs()
 
-        # candidate step structures: every transport, and for RCCL the fc-update carry on/off
-        # (cnn_step.CnnStep.fc_carry) unless PDM_FC_CARRY forces it
+        # candidate step structures: every transport, and for RCCL the fc-update placement
+        # (cnn_step.CnnStep.fc_carry / fc_side: carried past the next cnn_fwd, one grouped
+        # launch, or on a side stream) unless PDM_FC_CARRY forces it
         cands = []
         for name, red in reducers.items():
             if name == "rccl" and model == "cnn" and os.environ.get("PDM_FC_CARRY") is None:
-                cands += [("rccl", red, True), ("rccl-nocarry", red, False)]
+                cands += [("rccl", red, "carry"), ("rccl-nocarry", red, "nocarry"),
+                          ("rccl-side", red, "side")]
             else:
-                cands.append((name, red, os.environ.get("PDM_FC_CARRY", "1") != "0"))
+                env = os.environ.get("PDM_FC_CARRY", "1") != "0"
+                side = os.environ.get("PDM_FC_SIDE", "0") == "1"
+                cands.append((name, red, "side" if side and env else ("carry" if env else "nocarry")))
 
         opt.sync_hyperparams()
         next_epoch()

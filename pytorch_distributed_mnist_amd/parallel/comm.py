@@ -135,15 +135,19 @@ def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | No
     ev = torch.cuda.Event()
     ev.record()
     t0 = time.monotonic()
-    delay = 1e-5
+    delay = 0.0
     while not ev.query():
-        if time.monotonic() - t0 > timeout_s:
+        waited = time.monotonic() - t0
+        if waited > timeout_s:
             if isinstance(comm, RcclComm):
                 comm.abort()
             raise RuntimeError(f"{what} did not finish within {timeout_s:.0f} s (a peer rank is "
                                f"missing or hung); communicator aborted")
-        time.sleep(delay)
-        delay = min(delay * 2, 1e-3)
+        # spin for the first 50 ms (a timed window must not end with a sleep overshooting
+        # the device by up to the backoff step), then back off to 1 ms polls
+        if waited > 0.05:
+            delay = min(max(delay * 2, 1e-4), 1e-3)
+            time.sleep(delay)
     torch.cuda.synchronize(device)
 
 

@@ -178,6 +178,13 @@ class CnnStep(GpuStepBase):
         # when the transfer is short).  bench.py calibrates both; PDM_FC_CARRY=0/1 forces.
         env = os.environ.get("PDM_FC_CARRY")
         self.fc_carry = True if env is None else env != "0"
+        # ... or (fc_side, with fc_carry) run the fc-bucket update on a side stream as soon as
+        # its all-reduce lands, beside the conv update and the next cnn_fwd; the next fc1_fwd
+        # waits for it.  Worth it when those kernels leave CUs idle (small per-rank batches:
+        # cnn_fwd_band is 192 workgroups at B = 32 / 64); bench.py calibrates it as well.
+        self.fc_side = os.environ.get("PDM_FC_SIDE", "0") == "1"
+        self._side = None
+        self._side_ev = None
         self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
         self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
         self.refresh_shadows()
@@ -303,7 +310,9 @@ class CnnStep(GpuStepBase):
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
                   self.pmask, *self.fwd_outputs(B))
-        if carry_in:
+        if carry_in and self.fc_side:
+            torch.cuda.current_stream(self.device).wait_event(self._side_ev)
+        elif carry_in:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(self._bucket_segments()[0])
         C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
@@ -369,6 +378,19 @@ class CnnStep(GpuStepBase):
         b0, b1 = self._bucket_segments()
         self.reducer.bucket_ready(1)
         self.reducer.bucket_ready(0)
+        if self.fc_side:
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+                self._side_ev = torch.cuda.Event()
+            with torch.cuda.stream(self._side):
+                self.reducer.wait_bucket(0)          # the side stream waits for bucket 0
+                self.launch_optimizer(b0)
+                self._side_ev.record(self._side)
+            self.reducer.wait_bucket(1)
+            self.launch_optimizer(b1)
+            if not carry_out:                        # a graph ends with every stream joined
+                torch.cuda.current_stream(self.device).wait_event(self._side_ev)
+            return
         self.reducer.wait_bucket(1)
         self.launch_optimizer(b1)
         if not carry_out:

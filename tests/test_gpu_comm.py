@@ -74,24 +74,26 @@ def test_grad_reducer_grouped_all_ready(gpu):
     comm.close()
 
 
-@pytest.mark.parametrize("carry", [True, False])
-def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry):
+@pytest.mark.parametrize("carry", ["carry", "nocarry", "side"])
+@pytest.mark.parametrize("B", [256, 32])
+def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
     """The world_size > 1 step structure (unfused conv reduction, grouped RCCL all-reduce of
     both buckets, finalize) with a forced 1-rank RCCL communicator, graph-captured, gives
     the same parameters as the world_size-1 fast path."""
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.runtime.program import build_local_program
-    train = synthetic_split(256 * 9 + 40, True)
+    train = synthetic_split(B * 9 + 40, True)
     test = synthetic_split(256, False)
     out = []
     for force in (False, True):
         comm = _comm(gpu) if force else None
-        p = build_local_program("cnn", "bf16", "cuda", 256, train, test, optimizer="sgd", lr=0.05,
+        p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.05,
                                 momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=force,
                                 transport="rccl")
         assert p.gpu.fuse_conv_reduce == (not force)
-        p.gpu.fc_carry = carry
+        p.gpu.fc_carry = carry != "nocarry"
+        p.gpu.fc_side = carry == "side"
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         p.train_epoch()
