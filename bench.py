@@ -130,7 +130,7 @@ def main():
     train = synthetic_split(a.train_size, True)
     test = synthetic_split(1024, False)
     n = len(train)
-    prefetch = EpochIndexPrefetcher(n, ws, rank)
+    prefetch = EpochIndexPrefetcher(n, ws, rank, pin=True)
     first = next(iter(reducers.values()))
 
     def sync(what):
@@ -153,10 +153,14 @@ def main():
         state = {"epoch": 0, "step": 0}
 
         def next_epoch():
+            t_ne = time.perf_counter()
             prog.set_train_indices(prefetch.get(state["epoch"]))
             prog.gpu.begin_epoch()
             state["epoch"] += 1
             state["step"] = 0
+            if os.environ.get("PDM_BENCH_DEBUG"):
+                print(f"bench.py: next_epoch host {1e6 * (time.perf_counter() - t_ne):.0f} us",
+                      file=sys.stderr, flush=True)
 
         def run(k):
             while k > 0:
@@ -246,7 +250,7 @@ def main():
         # from the step that leaves K // 2 full steps before the boundary (every step is the
         # same kernel chain on a different batch of the sampler order)
         left = full - state["step"]
-        if a.steps >= 2 and left > a.steps // 2:
+        if a.steps >= 2 and left > a.steps // 2 and os.environ.get("PDM_BENCH_BOUNDARY", "1") != "0":
             skip = left - a.steps // 2
             sync("reposition")
             prog.gpu.ctr[0] += skip            # device data-step counter

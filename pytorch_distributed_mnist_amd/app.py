@@ -158,7 +158,8 @@ def run(args):
             return
 
         # epoch e+1's sample order is computed on a host thread while epoch e trains
-        prefetch = sampler.EpochIndexPrefetcher(len(train_split), world_size, rank)
+        prefetch = sampler.EpochIndexPrefetcher(len(train_split), world_size, rank,
+                                                pin=program.gpu is not None)
         for epoch in range(args.start_epoch, args.epochs):
             with trace.range("epoch {}".format(epoch)):
                 adjust_learning_rate(optimizer, epoch, args)

@@ -80,16 +80,26 @@ class EpochIndexPrefetcher:
     worker, so at an epoch boundary the host only uploads a ready vector and the GPU never
     idles behind the sampler.  torch ops release the GIL, so the worker overlaps the
     host's graph-replay loop.
+
+    With ``pin=True`` (GPU programs) the worker also converts the order to int32 in pinned
+    host memory, the form the device upload takes, so the boundary's host work is one async
+    copy (GpuStepBase.set_train_indices).
     """
 
-    def __init__(self, n: int, world_size: int, rank: int, **kw):
+    def __init__(self, n: int, world_size: int, rank: int, pin: bool = False, **kw):
         from concurrent.futures import ThreadPoolExecutor
         self.n, self.world_size, self.rank, self.kw = n, world_size, rank, kw
+        self.pin = pin
         self._ex = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pdm-sampler")
         self._next = None          # (epoch, future)
 
     def _compute(self, epoch: int) -> torch.Tensor:
-        return distributed_indices(self.n, self.world_size, self.rank, epoch, **self.kw)
+        idx = distributed_indices(self.n, self.world_size, self.rank, epoch, **self.kw)
+        if self.pin:
+            out = torch.empty(idx.numel(), dtype=torch.int32, pin_memory=True)
+            out.copy_(idx)
+            return out
+        return idx
 
     def get(self, epoch: int) -> torch.Tensor:
         if self._next is not None and self._next[0] == epoch:

@@ -71,27 +71,22 @@ class GpuStepBase:
     def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
         """Stream-ordered upload of the next epoch's sample order.
 
-        The copy goes from a pinned staging buffer with non_blocking=True, so the
-        host does not wait for the queued steps of the previous epoch: the copy
-        and the counter reset execute after them, in stream order.  Two staging
-        buffers alternate; an event guards reuse of the older one.
+        The copy is non_blocking from pinned host memory, so the host does not wait for the
+        queued steps of the previous epoch: the copy and the counter reset execute after
+        them, in stream order.  ``EpochIndexPrefetcher(pin=True)`` hands over a pinned int32
+        vector prepared on its worker thread (torch's caching host allocator keeps the block
+        alive until the copy has run); anything else is staged through a pinned buffer here.
         """
         n = idx_cpu.numel()
         if self.idx.numel() != n:
             self.idx = torch.empty(n, dtype=torch.int32, device=self.device)
             self.graphs.clear()          # graphs captured the old buffer address
-            self._staging = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(2)]
-            self._staging_ev = [None, None]
-            self._staging_i = 0
-        i = self._staging_i
-        if self._staging_ev[i] is not None:
-            self._staging_ev[i].synchronize()
-        self._staging[i].copy_(idx_cpu.to(torch.int32))
-        self.idx.copy_(self._staging[i], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._staging_ev[i] = ev
-        self._staging_i = 1 - i
+        if idx_cpu.dtype == torch.int32 and idx_cpu.is_pinned():
+            src = idx_cpu
+        else:
+            src = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            src.copy_(idx_cpu)
+        self.idx.copy_(src, non_blocking=True)
         self.ctr.zero_()
 
     def begin_epoch(self) -> None:

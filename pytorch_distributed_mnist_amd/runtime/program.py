@@ -44,6 +44,7 @@ class TrainProgram:
         self.test_split = test_split
         self.train_idx_cpu: Optional[torch.Tensor] = None
         self._bounds = []
+        self._n_train = 0
         # host sync before the once-per-epoch metric read: set by the app to a bounded
         # wait (parallel.bounded_sync) so a hung collective raises after --timeout
         self.sync_fn = None
@@ -57,26 +58,31 @@ class TrainProgram:
 
     # -- epochs ---------------------------------------------------------------
     def set_train_indices(self, indices: torch.Tensor) -> None:
-        """Install this rank's sample order for the coming epoch."""
+        """Install this rank's sample order for the coming epoch.
+
+        GPU: the vector goes to the device as is (the prefetcher hands over a pinned int32
+        tensor, so the boundary's host work is one async copy and two launches); the batch
+        bounds are arithmetic (full batches, then one ragged tail, as the DataLoader)."""
+        self._n_train = len(indices)
+        if self.gpu is not None:
+            self.gpu.set_train_indices(indices)
+            return
         self.train_idx_cpu = indices.to(torch.int64)
         self._bounds = batch_bounds(len(indices), self.batch_size)
-        if self.gpu is not None:
-            self.gpu.set_train_indices(self.train_idx_cpu)
 
     @property
     def steps_per_epoch(self) -> int:
-        return len(self._bounds)
+        return -(-self._n_train // self.batch_size)
 
     def train_epoch(self):
         self.metrics.reset(DeviceMetrics.TRAIN)
         self.optimizer.sync_hyperparams()
         if self.gpu is not None:
             self.gpu.begin_epoch()
-            sizes = [size for _, size in self._bounds]
-            full = sum(1 for s in sizes if s == self.batch_size)
+            full, tail = divmod(self._n_train, self.batch_size)
             self.gpu.train_steps(self.batch_size, full)      # full batches come first
-            for s in sizes[full:]:
-                self.gpu.train_step(s)                        # ragged tail
+            if tail:
+                self.gpu.train_step(tail)                     # ragged tail
             if self.sync_fn is not None:
                 self.sync_fn("training epoch")
         else:
