@@ -130,7 +130,7 @@ def main():
     train = synthetic_split(a.train_size, True)
     test = synthetic_split(1024, False)
     n = len(train)
-    prefetch = EpochIndexPrefetcher(n, ws, rank, pin=True)
+    prefetch = EpochIndexPrefetcher(n, ws, rank, int32=True)
     first = next(iter(reducers.values()))
 
     def sync(what):
@@ -152,21 +152,31 @@ def main():
         full = -(-n // ws) // B                    # full-batch steps per epoch
         state = {"epoch": 0, "step": 0}
 
+        dbg = os.environ.get("PDM_BENCH_DEBUG")
+        marks = []
+
+        def mark(what):
+            if dbg:
+                marks.append((what, time.perf_counter()))
+
         def next_epoch():
-            t_ne = time.perf_counter()
-            prog.set_train_indices(prefetch.get(state["epoch"]))
+            mark("get")
+            idx = prefetch.get(state["epoch"])
+            nxt = prefetch.peek(state["epoch"] + 1)
+            mark("gather")
+            prog.set_train_indices(idx, nxt)
+            mark("begin_epoch")
             prog.gpu.begin_epoch()
+            mark("boundary done")
             state["epoch"] += 1
             state["step"] = 0
-            if os.environ.get("PDM_BENCH_DEBUG"):
-                print(f"bench.py: next_epoch host {1e6 * (time.perf_counter() - t_ne):.0f} us",
-                      file=sys.stderr, flush=True)
 
         def run(k):
             while k > 0:
                 if state["step"] >= full:
                     next_epoch()
                 m = min(k, full - state["step"])
+                mark(f"replay {m}")
                 prog.gpu.train_steps(B, m)
                 state["step"] += m
                 k -= m
@@ -176,8 +186,15 @@ def main():
             barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            marks.clear()
             run(k)
+            mark("sync")
             sync("timed steps")
+            mark("end")
+            if dbg and rank == 0:
+                print("bench.py: window " + " | ".join(f"{w} @{1e6 * (t - t0):.0f}"
+                                                       for w, t in marks), file=sys.stderr,
+                      flush=True)
             barrier()
             torch.cuda.synchronize()
             return allmax(time.perf_counter() - t0)

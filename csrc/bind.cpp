@@ -157,24 +157,52 @@ void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
 }
 
 // ------------------------------------------------------------------ data
+// idx: the epoch's sample order, int32 -- a device tensor, or a pinned host tensor that the
+// kernel reads in place (zero-copy; the caller keeps it alive until the launch has run).
+// ctr (int64 device, optional): step counters reset to 0; step (int64[1], optional): set to
+// step_value (the optimizer step count, Adam's bias correction).
 void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tensor out_images,
-                  at::Tensor out_labels) {
+                  at::Tensor out_labels, c10::optional<at::Tensor> ctr, c10::optional<at::Tensor> step,
+                  int64_t step_value) {
   c10::DeviceGuard g(images.device());
   need(images, at::kByte, "images");
   need(labels, at::kInt, "labels");
-  need(idx, at::kInt, "idx");
   need(out_images, at::kByte, "out_images");
   need(out_labels, at::kInt, "out_labels");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous(), "idx must be contiguous int32");
+  const int32_t* ip = nullptr;
+  if (idx.is_cuda()) {
+    ip = idx.data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(idx.is_pinned(), "a host idx must be pinned (device-mapped) memory");
+    void* dp = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dp, idx.data_ptr(), 0);
+    TORCH_CHECK(e == hipSuccess && dp != nullptr, "hipHostGetDevicePointer: ", hipGetErrorString(e));
+    ip = static_cast<const int32_t*>(dp);
+  }
   TORCH_CHECK(images.dim() == 2 && images.size(1) == 784, "images must be [N, 784]");
   const int64_t n = idx.numel();
   TORCH_CHECK(out_images.numel() >= n * 784 && out_labels.numel() >= n, "output too small");
   need_aligned(images.data_ptr(), 16, "images");
   need_aligned(out_images.data_ptr(), 16, "out_images");
-  // indices are validated on the host by the caller (sampler output < N)
-  launch_gather_epoch(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
-                      idx.data_ptr<int32_t>(), (int)n, (int)images.size(0),
-                      out_images.data_ptr<uint8_t>(),
-                      out_labels.data_ptr<int32_t>(), cur_stream(images));
+  int64_t* cp = nullptr;
+  int nctr = 0;
+  if (ctr.has_value() && ctr->defined()) {
+    need(*ctr, at::kLong, "ctr");
+    TORCH_CHECK(ctr->numel() <= 256, "ctr: at most 256 counters");
+    cp = ptr<int64_t>(*ctr);
+    nctr = (int)ctr->numel();
+  }
+  int64_t* sp = nullptr;
+  if (step.has_value() && step->defined()) {
+    need(*step, at::kLong, "step");
+    sp = ptr<int64_t>(*step);
+  }
+  // indices are validated on the host by the caller (sampler output < N); bounds-check
+  // builds also check them in the kernel
+  launch_gather_epoch(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), ip, (int)n,
+                      (int)images.size(0), out_images.data_ptr<uint8_t>(),
+                      out_labels.data_ptr<int32_t>(), cp, nctr, sp, step_value, cur_stream(images));
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -757,7 +785,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("signal_ch") = -1, py::arg("waits") = std::vector<int64_t>{},
         py::arg("timeout_s") = 60.0, py::arg("bump") = py::none(),
         py::arg("metrics") = py::none());
-  m.def("gather_epoch", &gather_epoch);
+  m.def("gather_epoch", &gather_epoch, py::arg("images"), py::arg("labels"), py::arg("idx"),
+        py::arg("out_images"), py::arg("out_labels"), py::arg("ctr") = py::none(),
+        py::arg("step") = py::none(), py::arg("step_value") = 0);
   m.def("xgmi_wait", &xgmi_wait);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
   m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });

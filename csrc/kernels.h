@@ -30,7 +30,8 @@ void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, 
 
 // ---------------------------------------------------------------- data
 void launch_gather_epoch(const uint8_t* images, const int32_t* labels, const int32_t* idx, int n,
-                         int nimg, uint8_t* out_images, int32_t* out_labels, hipStream_t st);
+                         int nimg, uint8_t* out_images, int32_t* out_labels, int64_t* ctr,
+                         int nctr, int64_t* step, int64_t step_value, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer
 constexpr int OPT_ADAM = 0;

@@ -2,6 +2,11 @@
 // contiguous uint8 buffer once per epoch (47 MB at 60k samples, one streaming pass).
 // The step kernels then read their batch as rows [ctr*B, ctr*B + B) of that buffer:
 // one dependent load (the step counter) instead of counter -> index -> random row.
+//
+// The index vector is read straight from the pinned host buffer the sampler thread filled
+// (zero-copy over the host link, 240 KB once per epoch), and the launch also resets the
+// step counters: an epoch boundary is this one kernel on the compute stream, with no
+// copy-engine hand-off and no extra fill launches in front of the next step.
 #include "common.h"
 #include "kernels.h"
 
@@ -11,7 +16,12 @@ __global__ __launch_bounds__(256) void gather_epoch_kernel(const uint8_t* __rest
                                                            const int32_t* __restrict__ labels,
                                                            const int32_t* __restrict__ idx, int n,
                                                            int nimg, uint8_t* __restrict__ out_images,
-                                                           int32_t* __restrict__ out_labels) {
+                                                           int32_t* __restrict__ out_labels,
+                                                           int64_t* __restrict__ ctr, int nctr,
+                                                           int64_t* __restrict__ step,
+                                                           int64_t step_value) {
+  if (blockIdx.x == 0 && threadIdx.x < nctr) ctr[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && step != nullptr) *step = step_value;
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
   if (row >= n) return;
   const int src = idx[row];
@@ -25,8 +35,9 @@ __global__ __launch_bounds__(256) void gather_epoch_kernel(const uint8_t* __rest
 }  // namespace
 
 void launch_gather_epoch(const uint8_t* images, const int32_t* labels, const int32_t* idx, int n,
-                         int nimg, uint8_t* out_images, int32_t* out_labels, hipStream_t st) {
-  if (n <= 0) return;
-  gather_epoch_kernel<<<(n + 15) / 16, 256, 0, st>>>(images, labels, idx, n, nimg, out_images,
-                                                     out_labels);
+                         int nimg, uint8_t* out_images, int32_t* out_labels, int64_t* ctr,
+                         int nctr, int64_t* step, int64_t step_value, hipStream_t st) {
+  if (n <= 0 && nctr == 0 && step == nullptr) return;
+  gather_epoch_kernel<<<max((n + 15) / 16, 1), 256, 0, st>>>(images, labels, idx, n, nimg, out_images,
+                                                             out_labels, ctr, nctr, step, step_value);
 }

@@ -159,12 +159,14 @@ def run(args):
 
         # epoch e+1's sample order is computed on a host thread while epoch e trains
         prefetch = sampler.EpochIndexPrefetcher(len(train_split), world_size, rank,
-                                                pin=program.gpu is not None)
+                                                int32=program.gpu is not None)
         for epoch in range(args.start_epoch, args.epochs):
             with trace.range("epoch {}".format(epoch)):
                 adjust_learning_rate(optimizer, epoch, args)
 
-                train_loss, train_acc = trainer.train(prefetch.get(epoch))
+                nxt = prefetch.peek(epoch + 1) if program.gpu is not None and \
+                    epoch + 1 < args.epochs else None
+                train_loss, train_acc = trainer.train(prefetch.get(epoch), nxt)
                 reducer.check()             # xgmi: raise if a peer never arrived
                 test_loss, test_acc = trainer.evaluate()
 

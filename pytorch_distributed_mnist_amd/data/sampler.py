@@ -76,43 +76,54 @@ class EpochIndexPrefetcher:
     The reference reshuffles inside its loop (``set_epoch``, multi_proc_single_gpu.py:231)
     and its DataLoader workers index lazily; here the whole epoch order is one
     ``randperm`` (~1.3 ms for 60k on the host).  ``get(e)`` returns epoch e's order
-    (computed now if it was not prefetched) and immediately starts epoch e+1's on the
-    worker, so at an epoch boundary the host only uploads a ready vector and the GPU never
-    idles behind the sampler.  torch ops release the GIL, so the worker overlaps the
+    (computed now if it was not prefetched) and queues epochs e+1 .. e+depth on the
+    worker, so at an epoch boundary the host only hands over ready vectors (this epoch's,
+    and with ``peek(e+1)`` the next one's, whose gather the device then runs early) and
+    the GPU never idles behind the sampler.  torch ops release the GIL, so the worker overlaps the
     host's graph-replay loop.
 
-    With ``pin=True`` (GPU programs) the worker also converts the order to int32 in pinned
-    host memory, the form the device upload takes, so the boundary's host work is one async
-    copy (GpuStepBase.set_train_indices).
+    With ``int32=True`` (GPU programs) the worker also converts the order to int32, the
+    form the gather kernel reads.  The worker makes no HIP call (no pinned allocation): a
+    host-memory allocation from any thread would invalidate a graph capture running on the
+    main thread.
     """
 
-    def __init__(self, n: int, world_size: int, rank: int, pin: bool = False, **kw):
+    def __init__(self, n: int, world_size: int, rank: int, int32: bool = False, depth: int = 2,
+                 **kw):
         from concurrent.futures import ThreadPoolExecutor
         self.n, self.world_size, self.rank, self.kw = n, world_size, rank, kw
-        self.pin = pin
+        self.int32 = int32
+        self.depth = depth
         self._ex = ThreadPoolExecutor(max_workers=1, thread_name_prefix="pdm-sampler")
-        self._next = None          # (epoch, future)
+        self._futs = {}            # epoch -> future
 
     def _compute(self, epoch: int) -> torch.Tensor:
         idx = distributed_indices(self.n, self.world_size, self.rank, epoch, **self.kw)
-        if self.pin:
-            out = torch.empty(idx.numel(), dtype=torch.int32, pin_memory=True)
-            out.copy_(idx)
-            return out
-        return idx
+        return idx.to(torch.int32) if self.int32 else idx
+
+    def _future(self, epoch: int):
+        f = self._futs.get(epoch)
+        if f is None:
+            f = self._futs[epoch] = self._ex.submit(self._compute, epoch)
+        return f
 
     def get(self, epoch: int) -> torch.Tensor:
-        if self._next is not None and self._next[0] == epoch:
-            idx = self._next[1].result()
-        else:
-            if self._next is not None:
-                self._next[1].cancel()
-            idx = self._compute(epoch)
-        self._next = (epoch + 1, self._ex.submit(self._compute, epoch + 1))
+        """Epoch ``epoch``'s order; the next ``depth`` epochs' are then computed behind it."""
+        idx = self._future(epoch).result()
+        for e in list(self._futs):
+            if e < epoch:
+                self._futs.pop(e).cancel()
+        for e in range(epoch + 1, epoch + 1 + self.depth):
+            self._future(e)
         return idx
 
+    def peek(self, epoch: int) -> torch.Tensor:
+        """Epoch ``epoch``'s order (computed now if it was not prefetched), keeping it for
+        the later ``get``: lets the device start on the next epoch's gather early."""
+        return self._future(epoch).result()
+
     def close(self) -> None:
-        if self._next is not None:
-            self._next[1].cancel()
+        for f in self._futs.values():
+            f.cancel()
         self._ex.shutdown(wait=True)
-        self._next = None
+        self._futs = {}

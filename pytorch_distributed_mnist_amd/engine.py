@@ -25,16 +25,17 @@ class Trainer:
         if self.program.is_gpu:
             torch.cuda.synchronize(self.program.device)
 
-    def train(self, indices=None):
+    def train(self, indices=None, next_indices=None):
         """One training epoch.  ``indices``: this rank's sample order for the epoch (the
         reference's ``set_epoch`` reshuffle, :231), installed inside the timed region so the
-        epoch time includes the boundary work (index upload + epoch gather)."""
+        epoch time includes the boundary work (epoch gather).  ``next_indices``: the next
+        epoch's order, if known (its gather then runs beside this epoch's first steps)."""
         self._sync()
         t0 = time.perf_counter()
         with trace.range("train"):
             if indices is not None:
                 with trace.range("sampler upload"):
-                    self.program.set_train_indices(indices)
+                    self.program.set_train_indices(indices, next_indices)
             result = self.program.train_epoch()   # reading the metrics synchronises
         self.last_train_seconds = time.perf_counter() - t0
         return result

@@ -78,18 +78,6 @@ class CnnStepF32(GpuStepBase):
             # hand-off words; the fp32 program uses the transport's per-bucket launches
             self.reducer.streamed = False
         self._fused = {}
-        self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
-        self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
-
-    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
-        n = idx_cpu.numel()
-        if self.ep_images.numel() != n * 784:
-            self.ep_images = torch.empty(n * 784, dtype=torch.uint8, device=self.device)
-            self.ep_labels = torch.empty(n, dtype=torch.int32, device=self.device)
-            self.graphs.clear()
-        super().set_train_indices(idx_cpu)
-        self.C.gather_epoch(self.train_images, self.train_labels, self.idx,
-                            self.ep_images.view(n, 784), self.ep_labels)
 
     def refresh_shadows(self) -> None:
         """No bf16 operand copies in the fp32 program."""

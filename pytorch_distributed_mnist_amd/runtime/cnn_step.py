@@ -185,20 +185,7 @@ class CnnStep(GpuStepBase):
         self.fc_side = os.environ.get("PDM_FC_SIDE", "0") == "1"
         self._side = None
         self._side_ev = None
-        self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
-        self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
         self.refresh_shadows()
-
-    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
-        """Upload the epoch order, then materialise the epoch's samples contiguously."""
-        n = idx_cpu.numel()
-        if self.ep_images.numel() != n * 784:
-            self.ep_images = torch.empty(n * 784, dtype=torch.uint8, device=self.device)
-            self.ep_labels = torch.empty(n, dtype=torch.int32, device=self.device)
-            self.graphs.clear()
-        super().set_train_indices(idx_cpu)
-        self.C.gather_epoch(self.train_images, self.train_labels, self.idx,
-                            self.ep_images.view(n, 784), self.ep_labels)
 
     @torch.no_grad()
     def refresh_shadows(self) -> None:

@@ -55,7 +55,16 @@ class GpuStepBase:
         self.test_labels = prog.test_split.labels.to(device=dev, dtype=torch.int32).contiguous()
         # [train data step, (spare)]
         self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.idx = torch.zeros(0, dtype=torch.int32, device=dev)
+        # the epoch's samples in sampler order, double-buffered (set_train_indices): slot
+        # `self.slot` holds the running epoch, the other one is filled for the next epoch
+        self._ep = [(torch.empty(0, dtype=torch.uint8, device=dev),
+                     torch.empty(0, dtype=torch.int32, device=dev)) for _ in range(2)]
+        self.slot = 0
+        self._pending = None             # (pinned order, slot, event): next epoch's gather
+        self._side = None                # stream of the ahead-of-time gathers
+        self._ring = None                # pinned staging buffers of the epoch orders
+        self._ring_i = 0
+        self._step_written = None
         self.use_graphs = bool(use_graphs) and self.reducer.capturable
         self.graphs = {}
         self.bfull = prog.batch_size
@@ -68,30 +77,101 @@ class GpuStepBase:
         self.phase_period = 1
 
     # -- data ----------------------------------------------------------------
-    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
-        """Stream-ordered upload of the next epoch's sample order.
+    @property
+    def ep_images(self) -> torch.Tensor:
+        return self._ep[self.slot][0]
 
-        The copy is non_blocking from pinned host memory, so the host does not wait for the
-        queued steps of the previous epoch: the copy and the counter reset execute after
-        them, in stream order.  ``EpochIndexPrefetcher(pin=True)`` hands over a pinned int32
-        vector prepared on its worker thread (torch's caching host allocator keeps the block
-        alive until the copy has run); anything else is staged through a pinned buffer here.
+    @property
+    def ep_labels(self) -> torch.Tensor:
+        return self._ep[self.slot][1]
+
+    def _stage(self, idx: torch.Tensor) -> list:
+        """Copy an epoch order into the next pinned staging buffer of a ring of three ([buffer,
+        event]); the gather kernel reads it in place (zero-copy).  The buffers are allocated
+        once, on this thread and never during a graph capture (a host-memory allocation from
+        any thread would invalidate a capture), and one is reused only after the event behind
+        its previous reader has completed (at most two are in flight: this epoch's and the
+        next's)."""
+        n = idx.numel()
+        if self._ring is None or self._ring[0][0].numel() != n:
+            self._ring = [[torch.empty(n, dtype=torch.int32, pin_memory=True), None]
+                          for _ in range(3)]
+            self._ring_i = 0
+        buf = self._ring[self._ring_i]
+        self._ring_i = (self._ring_i + 1) % 3
+        if buf[1] is not None:
+            buf[1].synchronize()
+        buf[0].copy_(idx)
+        return buf
+
+    def _gather(self, src: torch.Tensor, slot: int, counters: bool) -> None:
+        n = src.numel()
+        img, lab = self._ep[slot]
+        self.C.gather_epoch(self.train_images, self.train_labels, src, img.view(n, 784), lab,
+                            self.ctr if counters else None,
+                            self.opt._step_dev if counters else None,
+                            int(self.opt.step_count))
+
+    def set_train_indices(self, idx_cpu: torch.Tensor, next_idx=None) -> None:
+        """Install this epoch's sample order; optionally start materialising the next one's.
+
+        ``gather_epoch`` copies the epoch's samples contiguously into an epoch buffer (the
+        step kernels read their rows behind one counter load), reading the order in place
+        from a pinned staging buffer (``EpochIndexPrefetcher`` computes it on its worker
+        thread; only this thread touches pinned memory).  The epoch buffer is double-buffered: with ``next_idx`` given, the next
+        epoch's gather is queued right away on a side stream into the other buffer, behind an
+        event that marks the end of the previous epoch's steps (the last reader of that
+        buffer), so it runs beside this epoch's first steps.  At the next boundary the
+        compute stream then only waits for that event and resets the step counters (one small
+        launch): the boundary costs the GPU almost nothing.  Graphs bake in a buffer address,
+        so they are keyed by the slot too.  The host never waits for queued steps.
         """
         n = idx_cpu.numel()
-        if self.idx.numel() != n:
-            self.idx = torch.empty(n, dtype=torch.int32, device=self.device)
-            self.graphs.clear()          # graphs captured the old buffer address
-        if idx_cpu.dtype == torch.int32 and idx_cpu.is_pinned():
-            src = idx_cpu
+        if self._ep[0][0].numel() != n * 784:
+            self._ep = [(torch.empty(n * 784, dtype=torch.uint8, device=self.device),
+                         torch.empty(n, dtype=torch.int32, device=self.device))
+                        for _ in range(2)]
+            self.graphs.clear()          # graphs captured the old buffer addresses
+            self._pending = None
+        cur = torch.cuda.current_stream(self.device)
+        p = self._pending
+        self._pending = None
+        if p is not None and p[0] is idx_cpu:
+            # gathered ahead on the side stream: wait for it, reset the counters
+            self.slot = p[1]
+            cur.wait_event(p[2])
+            self.C.gather_epoch(self.train_images, self.train_labels,
+                                torch.empty(0, dtype=torch.int32, device=self.device),
+                                self.ep_images.view(-1, 784), self.ep_labels, self.ctr,
+                                self.opt._step_dev, int(self.opt.step_count))
         else:
-            src = torch.empty(n, dtype=torch.int32, pin_memory=True)
-            src.copy_(idx_cpu)
-        self.idx.copy_(src, non_blocking=True)
-        self.ctr.zero_()
+            # first epoch (or the order gathered ahead was not this one): gather in stream
+            # order into the running slot, behind the previous epoch's steps
+            buf = self._stage(idx_cpu)
+            self._gather(buf[0], self.slot, True)
+            buf[1] = torch.cuda.Event()
+            buf[1].record(cur)
+        self._step_written = self.opt.step_count
+        if next_idx is not None and next_idx.numel() == n:
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            free = torch.cuda.Event()
+            free.record(cur)             # everything queued so far: the previous epoch's steps
+            buf = self._stage(next_idx)
+            other = 1 - self.slot
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(free)
+                self._gather(buf[0], other, False)
+                done = torch.cuda.Event()
+                done.record(self._side)
+            buf[1] = done
+            self._pending = (next_idx, other, done)
 
     def begin_epoch(self) -> None:
         self.opt.sync_hyperparams()
-        self.opt.sync_step()
+        if self._step_written != self.opt.step_count:
+            self.opt.sync_step()
+        self._step_written = None
 
     # -- step ------------------------------------------------------------------
     # One hipGraph replay costs ~10-16 us of host time (MI355X_MICROARCH.md price
@@ -104,7 +184,7 @@ class GpuStepBase:
 
     def _graph(self, B: int, nsteps: int, phase=None):
         phase = self.phase if phase is None else phase
-        key = (B, nsteps, phase)
+        key = (B, nsteps, phase, self.slot)
         g = self.graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
@@ -123,13 +203,21 @@ class GpuStepBase:
         self.phase = (self.phase + nsteps) % self.phase_period
 
     def prepare(self, B: int) -> None:
-        """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES), so no
-        capture or first-launch upload lands inside a timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
+        """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, both
+        step phases, both epoch buffers), so no capture or first-launch upload lands inside a
+        timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
         when replayed."""
         if not self.use_graphs:
             return
-        for n, ph in ((n, ph) for n in self.GRAPH_SIZES for ph in range(self.phase_period)):
-            g = self._graph(B, n, ph)
+        saved = self.slot
+        todo = [(n, ph, sl) for n in self.GRAPH_SIZES for ph in range(self.phase_period)
+                for sl in range(2)]
+        for n, ph, sl in todo:
+            self.slot = sl
+            try:
+                g = self._graph(B, n, ph)
+            finally:
+                self.slot = saved
             try:
                 exe = g.raw_cuda_graph_exec()
             except (AttributeError, RuntimeError):
@@ -244,20 +332,6 @@ class LinearStep(GpuStepBase):
         self.fuse_reduce = (not self.reducer.active and
                             os.environ.get("PDM_FUSE_LIN_REDUCE", "1") != "0")
         self._fused = {}
-        self.ep_images = torch.empty(0, dtype=torch.uint8, device=self.device)
-        self.ep_labels = torch.empty(0, dtype=torch.int32, device=self.device)
-
-    def set_train_indices(self, idx_cpu: torch.Tensor) -> None:
-        """Upload the epoch order, then materialise the epoch's samples contiguously (the
-        step kernel then reads its rows behind one counter load instead of two)."""
-        n = idx_cpu.numel()
-        if self.ep_images.numel() != n * 784:
-            self.ep_images = torch.empty(n * 784, dtype=torch.uint8, device=self.device)
-            self.ep_labels = torch.empty(n, dtype=torch.int32, device=self.device)
-            self.graphs.clear()
-        super().set_train_indices(idx_cpu)
-        self.C.gather_epoch(self.train_images, self.train_labels, self.idx,
-                            self.ep_images.view(n, 784), self.ep_labels)
 
     def invalidate_graphs(self) -> None:
         super().invalidate_graphs()

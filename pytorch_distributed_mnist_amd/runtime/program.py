@@ -57,15 +57,16 @@ class TrainProgram:
             self.gpu = None
 
     # -- epochs ---------------------------------------------------------------
-    def set_train_indices(self, indices: torch.Tensor) -> None:
-        """Install this rank's sample order for the coming epoch.
+    def set_train_indices(self, indices: torch.Tensor, next_indices=None) -> None:
+        """Install this rank's sample order for the coming epoch (and, on the GPU, start
+        materialising the next epoch's, ``next_indices``, beside this one's first steps).
 
-        GPU: the vector goes to the device as is (the prefetcher hands over a pinned int32
-        tensor, so the boundary's host work is one async copy and two launches); the batch
-        bounds are arithmetic (full batches, then one ragged tail, as the DataLoader)."""
+        GPU: the pinned int32 order the prefetcher hands over is read by the gather kernel in
+        place; the batch bounds are arithmetic (full batches, then one ragged tail, as the
+        DataLoader)."""
         self._n_train = len(indices)
         if self.gpu is not None:
-            self.gpu.set_train_indices(indices)
+            self.gpu.set_train_indices(indices, next_indices)
             return
         self.train_idx_cpu = indices.to(torch.int64)
         self._bounds = batch_bounds(len(indices), self.batch_size)

@@ -255,3 +255,33 @@ def test_fused_conv_reduce_matches_separate_pass(gpu):
     for other in res[1:]:
         for a, b in zip(res[0], other):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("model,dtype,opt", [("cnn", "bf16", "sgd"), ("linear", "fp32", "adam")])
+def test_epoch_gather_ahead_bit_identical(gpu, model, dtype, opt):
+    """Double-buffered epoch buffer: with the next epoch's order handed over early
+    (set_train_indices(idx, next_idx)), its gather runs on a side stream beside the current
+    epoch's steps and the boundary only resets the counters.  Four epochs (graphs, ragged
+    tails, both buffer slots twice, a pinned order from the prefetcher) must give the same
+    bits as installing every epoch in stream order, and the device step count must follow."""
+    from pytorch_distributed_mnist_amd.data.sampler import EpochIndexPrefetcher
+    train = synthetic_split(96 * 5 + 40, True)
+    test = synthetic_split(256, False)
+    res = []
+    for ahead in (False, True):
+        p = build_local_program(model, dtype, "cuda", 96, train, test, optimizer=opt, lr=0.02,
+                                seed=7, use_graphs=True)
+        p.optimizer.sync_hyperparams()
+        pf = EpochIndexPrefetcher(len(train), 1, 0, int32=True)
+        losses = []
+        for ep in range(4):
+            nxt = pf.peek(ep + 1) if ahead and ep < 3 else None
+            p.set_train_indices(pf.get(ep), nxt)
+            tl, _ = p.train_epoch()
+            losses.append(tl.average)
+            assert int(p.gpu.opt._step_dev.item()) == p.optimizer.step_count
+        pf.close()
+        torch.cuda.synchronize()
+        res.append((p.arena.params.clone(), losses))
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
