@@ -61,7 +61,7 @@ class GpuStepBase:
                      torch.empty(0, dtype=torch.int32, device=dev)) for _ in range(2)]
         self.slot = 0
         self._pending = None             # (pinned order, slot, event): next epoch's gather
-        self._side = None                # stream of the ahead-of-time gathers
+        self._gather_stream = None       # stream of the ahead-of-time gathers
         self._ring = None                # pinned staging buffers of the epoch orders
         self._ring_i = 0
         self._step_written = None
@@ -153,17 +153,17 @@ class GpuStepBase:
             buf[1].record(cur)
         self._step_written = self.opt.step_count
         if next_idx is not None and next_idx.numel() == n:
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
+            if self._gather_stream is None:
+                self._gather_stream = torch.cuda.Stream(self.device)
             free = torch.cuda.Event()
             free.record(cur)             # everything queued so far: the previous epoch's steps
             buf = self._stage(next_idx)
             other = 1 - self.slot
-            with torch.cuda.stream(self._side):
-                self._side.wait_event(free)
+            with torch.cuda.stream(self._gather_stream):
+                self._gather_stream.wait_event(free)
                 self._gather(buf[0], other, False)
                 done = torch.cuda.Event()
-                done.record(self._side)
+                done.record(self._gather_stream)
             buf[1] = done
             self._pending = (next_idx, other, done)
 
