@@ -509,7 +509,7 @@ static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   u.kind = -1;
   if (!t.has_value()) return u;
   const py::tuple& a = *t;
-  TORCH_CHECK(a.size() == 16 || a.size() == 17, "fc_update: 16 or 17 entries");
+  TORCH_CHECK(a.size() >= 16 && a.size() <= 18, "fc_update: 16 to 18 entries");
   u.kind = (int)a[0].cast<int64_t>();
   TORCH_CHECK(u.kind == OPT_SGD, "fc_update: SGD-momentum only (Adam runs in the optimizer kernel)");
   auto p = a[1].cast<at::Tensor>(), g = a[2].cast<at::Tensor>(), m = a[3].cast<at::Tensor>();
@@ -543,7 +543,8 @@ static FcUpdate make_fc_update(const c10::optional<py::tuple>& t) {
   u.nesterov = a[14].cast<bool>() ? 1 : 0;
   u.grad_scale = (float)a[15].cast<double>();
   u.shadow_t_next = nullptr;
-  if (a.size() == 17 && !a[16].is_none()) {
+  u.store_grad = (a.size() == 18 && !a[17].is_none()) ? (a[17].cast<bool>() ? 1 : 0) : 1;
+  if (a.size() >= 17 && !a[16].is_none()) {
     auto t2 = a[16].cast<at::Tensor>();
     need(t2, at::kBFloat16, "fc shadow_t_next");
     TORCH_CHECK(t2.numel() == u.numel, "fc_update: shadow_t_next is one W1^T copy");

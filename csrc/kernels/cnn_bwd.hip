@@ -170,14 +170,16 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       }
     }
     FC_STAMP(bid, 11);
+    if (fcu.kind < 0 || fcu.store_grad) {
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = wave * 32 + mt * 16 + 4 * g + r;
+        for (int r = 0; r < 4; ++r) {
+          const int n = wave * 32 + mt * 16 + 4 * g + r;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + 16 * nt + i16] = acc[mt][nt][r];
-      }
+          for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + 16 * nt + i16] = acc[mt][nt][r];
+        }
+    }
     if (fcu.kind >= 0) {
       // world size 1 (kernels.h FcUpdate): the SGD-momentum update of this tile, from the
       // gradient still in registers; writes the fp32 weight, the momentum and the bf16 [n][k]

@@ -170,6 +170,10 @@ class CnnStep(GpuStepBase):
         # one half while its weight tiles write the other), so the optimizer launch skips fc1
         # entirely (PDM_FC1_WT2=0: the optimizer re-derives W1^T instead)
         self.wt_double = os.environ.get("PDM_FC1_WT2", "1") != "0"
+        # the fused fc1 update consumes the fc1-weight gradient in registers; it is stored to
+        # the gradient arena only when something will read it (tests comparing gradients set
+        # keep_grads; PDM_KEEP_GRADS=1 forces it): 4.7 MB of writes per step otherwise
+        self.keep_grads = os.environ.get("PDM_KEEP_GRADS", "0") == "1"
         self.phase_period = 2 if self._wt_double_on() else 1
         self._fused = {}
         # RCCL data plane: defer the fc-bucket update past the next step's cnn_fwd so the
@@ -394,7 +398,7 @@ class CnnStep(GpuStepBase):
                 o.momentum_buffer[off:off + n], None, self.wf1, o._lr_dev, o._step_dev, 0.0, 0.0,
                 0.0, float(g["weight_decay"]), float(g["momentum"]), float(g["dampening"]),
                 bool(g["nesterov"]), float(self.reducer.grad_scale),
-                self.wf1t2[1 - self.phase] if self._wt_double_on() else None)
+                self.wf1t2[1 - self.phase] if self._wt_double_on() else None, self.keep_grads)
 
     def _wt_double_on(self) -> bool:
         return self.fuse_fc1 and self.fuse_conv_reduce and self.wt_double

@@ -32,6 +32,7 @@ def _program(B, opt="sgd", lr=0.0, graphs=False, n=600, seed=0):
                                weight_decay=0.0 if lr == 0.0 else 1e-4, seed=seed,
                                use_graphs=graphs)
     prog.optimizer.sync_hyperparams()
+    prog.gpu.keep_grads = True     # these tests read the gradient arena
     return prog, train, test
 
 
