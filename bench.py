@@ -152,6 +152,17 @@ def main():
         full = -(-n // ws) // B                    # full-batch steps per epoch
         state = {"epoch": 0, "step": 0}
 
+        cut = {}
+
+        def order(e):
+            """Epoch e's order, full batches only: the bench times full steps, so its epochs
+            are the sampler order without the ragged tail (one object per epoch: the program
+            recognises the order it gathered ahead by identity)."""
+            if e not in cut:
+                cut[e] = prefetch.peek(e)[:full * B]
+                cut.pop(e - 3, None)
+            return cut[e]
+
         dbg = os.environ.get("PDM_BENCH_DEBUG")
         marks = []
 
@@ -161,8 +172,10 @@ def main():
 
         def next_epoch():
             mark("get")
-            idx = prefetch.get(state["epoch"])
-            nxt = prefetch.peek(state["epoch"] + 1)
+            prefetch.get(state["epoch"])          # queues the following epochs' orders
+            idx = order(state["epoch"])
+            nxt = order(state["epoch"] + 1) if \
+                os.environ.get("PDM_GATHER_AHEAD", "1") != "0" else None
             mark("gather")
             prog.set_train_indices(idx, nxt)
             mark("begin_epoch")
@@ -270,10 +283,13 @@ def main():
         if a.steps >= 2 and left > a.steps // 2 and os.environ.get("PDM_BENCH_BOUNDARY", "1") != "0":
             skip = left - a.steps // 2
             sync("reposition")
-            prog.gpu.ctr[0] += skip            # device data-step counter
+            prog.gpu.skip_steps(skip)          # device data-step counter
             state["step"] += skip
         left = full - state["step"]
         boundaries = -(-(a.steps - left) // full) if a.steps > left else 0
+        if os.environ.get("PDM_BENCH_PRECOMPUTE") == "1":   # diagnostic: no sampler work in the window
+            for e in range(state["epoch"], state["epoch"] + 4):
+                prefetch.peek(e)
         elapsed = timed(a.steps)
         chosen.check()
         if not torch.isfinite(arena.params).all():

@@ -73,14 +73,25 @@ void check_data(const at::Tensor& images, const at::Tensor& labels, const at::Te
   // kernels' reads idx[ctr*bfull + i] stay in range.
 }
 
+// Epoch-buffer geometry of the step kernels (kernels.h StepRows): spe > 0 = the buffer holds
+// two epochs of nrow / 2 rows each, a step's rows follow from the running counter.
+StepRows step_rows(int64_t bfull, int64_t spe, int64_t nrow) {
+  if (spe > 0)
+    TORCH_CHECK(nrow % 2 == 0 && (spe - 1) * bfull < nrow / 2 && spe * bfull >= nrow / 2,
+                "epoch geometry: ", spe, " steps of ", bfull, " rows do not cover an epoch of ",
+                nrow / 2, " rows");
+  return StepRows{(int)bfull, (int)spe};
+}
+
 // ------------------------------------------------------------------ linear
 // idx None: epoch-buffer mode, the step's rows are images[ctr*bfull + i] (the host keeps ctr
 // within the buffer); otherwise the sampler gather images[idx[ctr*bfull + i]].
 void lin_train(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx, at::Tensor ctr,
                int64_t bfull, int64_t B, at::Tensor W, at::Tensor b, at::Tensor slab,
-               c10::optional<at::Tensor> metrics, c10::optional<at::Tensor> c1) {
+               c10::optional<at::Tensor> metrics, c10::optional<at::Tensor> c1, int64_t spe) {
   c10::DeviceGuard g(images.device());
   const bool gather = idx.has_value() && idx->defined();
+  TORCH_CHECK(!(gather && spe > 0), "an epoch geometry needs the epoch buffer (idx None)");
   int64_t nrow;
   if (gather) {
     check_data(images, labels, *idx, ctr, bfull, B);
@@ -112,7 +123,7 @@ void lin_train(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> i
   }
   launch_lin_train(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(),
                    gather ? idx->data_ptr<int32_t>() : nullptr, nrow, ctr.data_ptr<int64_t>(),
-                   (int)bfull, (int)B, W.data_ptr<float>(), b.data_ptr<float>(),
+                   step_rows(bfull, spe, nrow), (int)B, W.data_ptr<float>(), b.data_ptr<float>(),
                    slab.data_ptr<float>(), mp, opt_i64(c1), cur_stream(images));
 }
 
@@ -163,7 +174,7 @@ void lin_eval(at::Tensor images, at::Tensor labels, at::Tensor W, at::Tensor b,
 // step_value (the optimizer step count, Adam's bias correction).
 void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tensor out_images,
                   at::Tensor out_labels, c10::optional<at::Tensor> ctr, c10::optional<at::Tensor> step,
-                  int64_t step_value) {
+                  int64_t step_value, int64_t max_wgs) {
   c10::DeviceGuard g(images.device());
   need(images, at::kByte, "images");
   need(labels, at::kInt, "labels");
@@ -202,7 +213,8 @@ void gather_epoch(at::Tensor images, at::Tensor labels, at::Tensor idx, at::Tens
   // builds also check them in the kernel
   launch_gather_epoch(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), ip, (int)n,
                       (int)images.size(0), out_images.data_ptr<uint8_t>(),
-                      out_labels.data_ptr<int32_t>(), cp, nctr, sp, step_value, cur_stream(images));
+                      out_labels.data_ptr<int32_t>(), cp, nctr, sp, step_value, (int)max_wgs,
+                      cur_stream(images));
 }
 
 // ------------------------------------------------------------------ optimizer
@@ -376,7 +388,7 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
              c10::optional<at::Tensor> ctr, int64_t bfull, int64_t B, at::Tensor w1, at::Tensor b1,
              at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
              c10::optional<at::Tensor> xg, at::Tensor ylab, int64_t bands,
-             c10::optional<at::Tensor> a1g, c10::optional<at::Tensor> xng) {
+             c10::optional<at::Tensor> a1g, c10::optional<at::Tensor> xng, int64_t spe) {
   c10::DeviceGuard g(images.device());
   TORCH_CHECK(bands == 1 || bands == 2 || bands == 3 || bands == 6, "bands must be 1, 2, 3 or 6");
   const bool gather = idx.has_value() && idx->defined();
@@ -434,13 +446,13 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
       pxn = ptr<__bf16>(*xng);
     }
     launch_cnn_fwd_band(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
-                        (int)bfull, (int)B, (int)bands, w1.data_ptr<float>(), b1.data_ptr<float>(),
+                        step_rows(bfull, pidx ? 0 : spe, nrow), (int)B, (int)bands, w1.data_ptr<float>(), b1.data_ptr<float>(),
                         ptr<__bf16>(w2), b2.data_ptr<float>(), ptr<__bf16>(pool),
                         pmask.data_ptr<uint8_t>(), pa1, pxn, pxg, ylab.data_ptr<int32_t>(),
                         cur_stream(images));
   } else {
     launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
-                   (int)bfull, (int)B, w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2),
+                   step_rows(bfull, pidx ? 0 : spe, nrow), (int)B, w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2),
                    b2.data_ptr<float>(), ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(), pxg,
                    ylab.data_ptr<int32_t>(), cur_stream(images));
   }
@@ -649,7 +661,7 @@ int64_t cnn_bwd_nblk(int64_t B, int64_t ipb, int64_t bands) { return conv_blocks
 void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr, int64_t bfull,
              int64_t B, at::Tensor w1, at::Tensor b1, at::Tensor w2, at::Tensor b2,
              at::Tensor pool, c10::optional<at::Tensor> pmask, c10::optional<at::Tensor> a1g,
-             c10::optional<at::Tensor> xng, at::Tensor ylab) {
+             c10::optional<at::Tensor> xng, at::Tensor ylab, int64_t spe) {
   c10::DeviceGuard g(images.device());
   need(images, at::kByte, "images");
   need(labels, at::kInt, "labels");
@@ -678,7 +690,8 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
     need_aligned(xng->data_ptr(), 16, "xng");
   }
   launch_f32_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), images.size(0),
-                 ctr.has_value() ? ctr->data_ptr<int64_t>() : nullptr, (int)bfull, (int)B,
+                 ctr.has_value() ? ctr->data_ptr<int64_t>() : nullptr,
+                 step_rows(bfull, ctr.has_value() ? spe : 0, images.size(0)), (int)B,
                  w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                  pool.data_ptr<float>(), train ? pmask->data_ptr<uint8_t>() : nullptr,
                  train ? a1g->data_ptr<float>() : nullptr, train ? xng->data_ptr<float>() : nullptr,
@@ -775,7 +788,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("XG_LOC_DONE") = XG_LOC_DONE;
   m.def("lin_train", &lin_train, py::arg("images"), py::arg("labels"), py::arg("idx"),
         py::arg("ctr"), py::arg("bfull"), py::arg("B"), py::arg("W"), py::arg("b"), py::arg("slab"),
-        py::arg("metrics") = py::none(), py::arg("c1") = py::none());
+        py::arg("metrics") = py::none(), py::arg("c1") = py::none(), py::arg("spe") = 0);
   m.def("lin_reduce", &lin_reduce, py::arg("slab"), py::arg("B"), py::arg("gW"), py::arg("gb"),
         py::arg("c0") = py::none(), py::arg("xg") = py::none(), py::arg("metrics") = py::none());
   m.def("lin_eval", &lin_eval);
@@ -788,7 +801,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("metrics") = py::none());
   m.def("gather_epoch", &gather_epoch, py::arg("images"), py::arg("labels"), py::arg("idx"),
         py::arg("out_images"), py::arg("out_labels"), py::arg("ctr") = py::none(),
-        py::arg("step") = py::none(), py::arg("step_value") = 0);
+        py::arg("step") = py::none(), py::arg("step_value") = 0, py::arg("max_wgs") = 0);
   m.def("xgmi_wait", &xgmi_wait);
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
   m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });
@@ -800,7 +813,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_fwd", &cnn_fwd, py::arg("images"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
         py::arg("bfull"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1,
-        py::arg("a1g") = py::none(), py::arg("xng") = py::none());
+        py::arg("a1g") = py::none(), py::arg("xng") = py::none(), py::arg("spe") = 0);
   m.def("fc1_fwd", &fc1_fwd);
   m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
@@ -817,7 +830,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_reduce", &conv_reduce);
   m.def("f32_fwd", &f32_fwd, py::arg("images"), py::arg("labels"), py::arg("ctr"), py::arg("bfull"),
         py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"), py::arg("pool"),
-        py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"));
+        py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"), py::arg("spe") = 0);
   m.def("f32_fc1_fwd", &f32_fc1_fwd);
   m.def("f32_fc1_bwd", &f32_fc1_bwd);
   m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),

@@ -5,6 +5,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+
+// A training step's rows in the epoch buffer.  The data-step counter c runs on across epochs
+// (nothing resets it at an epoch boundary); with spe > 0 steps per epoch the buffer holds two
+// epochs, epoch e = c / spe in half e & 1 (rows [(e & 1) * nrow / 2, ...)), so the next
+// epoch's samples are gathered into the other half while this one trains and the step graphs
+// never change.  spe == 0: one flat buffer, row c * bfull + img.
+struct StepRows {
+  int bfull;   // full batch: the row stride between consecutive steps
+  int spe;     // steps per epoch (0: flat buffer)
+};
+__host__ __device__ __forceinline__ int64_t step_row(const StepRows g, int64_t nrow, int64_t c,
+                                                     int img) {
+  if (g.spe <= 0) return c * g.bfull + img;
+  const uint32_t e = (uint32_t)c / (uint32_t)g.spe;
+  const int64_t s = c - (int64_t)e * g.spe;
+  return (int64_t)(e & 1u) * (nrow >> 1) + s * g.bfull + img;
+}
+
 // ---------------------------------------------------------------- linear model
 constexpr int LIN_K = 784;
 constexpr int LIN_N = 10;
@@ -19,7 +37,7 @@ constexpr int LIN_EVAL_ROWS = 16;
 // sampler gather images[idx[ctr*bfull + i]].  metrics (fp64 [3]) and c1 (optimizer-step
 // counter, advanced once) are optional.
 void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                      int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W, const float* b,
+                      int64_t nrow, const int64_t* ctr, StepRows sr, int B, const float* W, const float* b,
                       float* slab, double* metrics, int64_t* c1, hipStream_t st);
 // metrics (optional): one extra workgroup sums the loss / correct slab columns into
 // metrics[0..1] in a fixed order (lin_train only adds the sample count)
@@ -31,7 +49,7 @@ void launch_lin_eval(const uint8_t* images, const int32_t* labels, int n_total, 
 // ---------------------------------------------------------------- data
 void launch_gather_epoch(const uint8_t* images, const int32_t* labels, const int32_t* idx, int n,
                          int nimg, uint8_t* out_images, int32_t* out_labels, int64_t* ctr,
-                         int nctr, int64_t* step, int64_t step_value, hipStream_t st);
+                         int nctr, int64_t* step, int64_t step_value, int max_wgs, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer
 constexpr int OPT_ADAM = 0;
@@ -163,7 +181,7 @@ constexpr int CNN_CONV_SLAB_DW1 = 18496;   // dW1 [32][9]
 constexpr int CNN_CONV_SLAB_DB1 = 18784;   // db1 [32]
 
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                    int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
+                    int64_t nrow, const int64_t* ctr, StepRows sr, int B, const float* w1, const float* b1,
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
                     int32_t* ylab, hipStream_t st);
 // small batches: each image over `bands` in {2, 3, 6} workgroups of 24 / bands conv2 rows
@@ -171,7 +189,7 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
 // image and the normalised x for cnn_bwd_band (a1g, xng) and / or the gathered uint8 image for
 // cnn_bwd (xg)
 void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                         int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
+                         int64_t nrow, const int64_t* ctr, StepRows sr, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
                          __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, uint8_t* xg,
                          int32_t* ylab, hipStream_t st);
@@ -205,7 +223,7 @@ void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, flo
 // a1g [B][676][32] and xng [B][784] carry the forward's conv1 activations and normalised
 // image to the backward; dh32 [ldt][128] is cnn_head's fp32 dh (launch_cnn_head dh32 != null).
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
-                    int bfull, int B, const float* w1, const float* b1, const float* w2,
+                    StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
                     int32_t* ylab, hipStream_t st);
 void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,

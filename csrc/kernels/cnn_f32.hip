@@ -44,7 +44,7 @@ __device__ __forceinline__ int w2h_off(int k, int c) { return k * 32 + (c ^ ((k 
 template <bool TRAIN>
 __global__ __launch_bounds__(FT, 1) void f32_fwd_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels, int64_t nrow,
-    const int64_t* __restrict__ ctr, int bfull, const float* __restrict__ w1,
+    const int64_t* __restrict__ ctr, const StepRows sr, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
     float* __restrict__ pool, uint8_t* __restrict__ pmask, float* __restrict__ a1g,
     float* __restrict__ xng, int32_t* __restrict__ ylab) {
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(FT, 1) void f32_fwd_kernel(
                                : reinterpret_cast<const float4*>(b2)[wt - 80];
     reinterpret_cast<float4*>(ws)[wt] = q;
   }
-  const int64_t row = min(ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img, nrow - 1);
+  const int64_t row = min(ctr ? step_row(sr, nrow, *ctr, img) : (int64_t)img, nrow - 1);
   if (tid < 196) {
     const uint32_t v = reinterpret_cast<const uint32_t*>(images + row * 784)[tid];
     const float4 x = make_float4(pdm_normalize(v & 0xff), pdm_normalize((v >> 8) & 0xff),
@@ -576,14 +576,14 @@ __global__ __launch_bounds__(FT, 1) void f32_conv_bwd_kernel(
 }  // namespace
 
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
-                    int bfull, int B, const float* w1, const float* b1, const float* w2,
+                    StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
                     int32_t* ylab, hipStream_t st) {
   if (a1g != nullptr)
-    f32_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, bfull, w1, b1, w2, b2, pool,
+    f32_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2, pool,
                                            pmask, a1g, xng, ylab);
   else
-    f32_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, bfull, w1, b1, w2, b2, pool,
+    f32_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2, pool,
                                             pmask, a1g, xng, ylab);
 }
 

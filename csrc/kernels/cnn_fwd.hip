@@ -53,7 +53,7 @@ static_assert(2 * F_TOTAL <= 163840 && F_A1 % 128 == 0, "cnn_fwd LDS carve");
 template <bool TRAIN>
 __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
+    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, const StepRows sr,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
     uint8_t* __restrict__ xg, int32_t* __restrict__ ylab) {
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   // anything else so its latency is not queued behind the weight loads.
   // sample row: sampler index (idx), epoch-buffer row (ctr only) or plain row (eval)
   // (clamped to the row space: a counter driven past the epoch reads a valid row)
-  const int64_t row_u = ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img;
+  const int64_t row_u = ctr ? step_row(sr, nrow, *ctr, img) : (int64_t)img;
   PDM_CHECK(row_u < nrow, "cnn_fwd sample row past the epoch", row_u, nrow);
   const int64_t row = min(row_u, nrow - 1);
   const int64_t src = idx ? (int64_t)idx[row] : row;
@@ -547,14 +547,14 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
 
 #if PDM_WANT_FWD_REST
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                    int64_t nrow, const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
+                    int64_t nrow, const int64_t* ctr, StepRows sr, int B, const float* w1, const float* b1,
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
                     int32_t* ylab, hipStream_t st) {
   if (xg != nullptr)
-    cnn_fwd_kernel<true><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1, w2,
+    cnn_fwd_kernel<true><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1, w2,
                                                     b2, pool, pmask, xg, ylab);
   else
-    cnn_fwd_kernel<false><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1, w2,
+    cnn_fwd_kernel<false><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1, w2,
                                                      b2, pool, pmask, xg, ylab);
 }
 

@@ -44,7 +44,7 @@ struct FwdBand {
 template <int R, bool TRAIN>
 __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
+    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, const StepRows sr,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
     bf16* __restrict__ a1g, bf16* __restrict__ xng, uint8_t* __restrict__ xg,
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
   }
   __builtin_amdgcn_sched_barrier(0);
   // 1. the dependent chain: counter -> sample row -> this band's x rows
-  const int64_t row_u = ctr ? (*ctr) * (int64_t)bfull + img : (int64_t)img;
+  const int64_t row_u = ctr ? step_row(sr, nrow, *ctr, img) : (int64_t)img;
   PDM_CHECK(row_u < nrow, "cnn_fwd_band sample row past the epoch", row_u, nrow);
   const int64_t row = min(row_u, nrow - 1);
   const int64_t src = idx ? (int64_t)idx[row] : row;
@@ -246,36 +246,36 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
 
 template <int R>
 void launch_band(const uint8_t* images, const int32_t* labels, const int32_t* idx, int64_t nrow,
-                 const int64_t* ctr, int bfull, int B, const float* w1, const float* b1,
+                 const int64_t* ctr, StepRows sr, int B, const float* w1, const float* b1,
                  const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, __bf16* a1g,
                  __bf16* xng, uint8_t* xg, int32_t* ylab, hipStream_t st) {
   const int nblk = B * FwdBand<R>::S;
   if (a1g != nullptr || xg != nullptr)
-    cnn_fwd_band_kernel<R, true><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1, b1,
+    cnn_fwd_band_kernel<R, true><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1,
                                                        w2, b2, pool, pmask, a1g, xng, xg, ylab);
   else
-    cnn_fwd_band_kernel<R, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, bfull, w1,
+    cnn_fwd_band_kernel<R, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1,
                                                         b1, w2, b2, pool, pmask, a1g, xng, xg, ylab);
 }
 
 }  // namespace
 
 void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                         int64_t nrow, const int64_t* ctr, int bfull, int B, int bands,
+                         int64_t nrow, const int64_t* ctr, StepRows sr, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
                          __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, uint8_t* xg,
                          int32_t* ylab, hipStream_t st) {
   switch (bands) {
     case 2:
-      launch_band<12>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
+      launch_band<12>(images, labels, idx, nrow, ctr, sr, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
                       xg, ylab, st);
       break;
     case 3:
-      launch_band<8>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
+      launch_band<8>(images, labels, idx, nrow, ctr, sr, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
                      xg, ylab, st);
       break;
     case 6:
-      launch_band<4>(images, labels, idx, nrow, ctr, bfull, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
+      launch_band<4>(images, labels, idx, nrow, ctr, sr, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
                      xg, ylab, st);
       break;
     default:

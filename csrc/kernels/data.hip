@@ -22,22 +22,25 @@ __global__ __launch_bounds__(256) void gather_epoch_kernel(const uint8_t* __rest
                                                            int64_t step_value) {
   if (blockIdx.x == 0 && threadIdx.x < nctr) ctr[threadIdx.x] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0 && step != nullptr) *step = step_value;
-  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
-  if (row >= n) return;
-  const int src = idx[row];
-  PDM_CHECK(src >= 0 && src < nimg, "gather_epoch index", src, nimg);
-  const uint4* s = reinterpret_cast<const uint4*>(images + (int64_t)src * 784);
-  uint4* d = reinterpret_cast<uint4*>(out_images + (int64_t)row * 784);
-  for (int c = threadIdx.x & 15; c < 49; c += 16) d[c] = s[c];
-  if ((threadIdx.x & 15) == 0) out_labels[row] = labels[src];
+  // 16 rows per workgroup pass; a grid smaller than the row count strides over the rest
+  for (int row = blockIdx.x * 16 + (threadIdx.x >> 4); row < n; row += gridDim.x * 16) {
+    const int src = idx[row];
+    PDM_CHECK(src >= 0 && src < nimg, "gather_epoch index", src, nimg);
+    const uint4* s = reinterpret_cast<const uint4*>(images + (int64_t)src * 784);
+    uint4* d = reinterpret_cast<uint4*>(out_images + (int64_t)row * 784);
+    for (int c = threadIdx.x & 15; c < 49; c += 16) d[c] = s[c];
+    if ((threadIdx.x & 15) == 0) out_labels[row] = labels[src];
+  }
 }
 
 }  // namespace
 
 void launch_gather_epoch(const uint8_t* images, const int32_t* labels, const int32_t* idx, int n,
                          int nimg, uint8_t* out_images, int32_t* out_labels, int64_t* ctr,
-                         int nctr, int64_t* step, int64_t step_value, hipStream_t st) {
+                         int nctr, int64_t* step, int64_t step_value, int max_wgs, hipStream_t st) {
   if (n <= 0 && nctr == 0 && step == nullptr) return;
-  gather_epoch_kernel<<<max((n + 15) / 16, 1), 256, 0, st>>>(images, labels, idx, n, nimg, out_images,
+  int grid = max((n + 15) / 16, 1);
+  if (max_wgs > 0 && grid > max_wgs) grid = max_wgs;
+  gather_epoch_kernel<<<grid, 256, 0, st>>>(images, labels, idx, n, nimg, out_images,
                                                              out_labels, ctr, nctr, step, step_value);
 }

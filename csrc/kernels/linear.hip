@@ -122,7 +122,7 @@ __device__ __forceinline__ float row_xent(const float (&lg)[N], int y, float (&p
 
 __global__ __launch_bounds__(THREADS) void lin_train_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, int bfull,
+    const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, const StepRows sr,
     int B, const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ slab,
     double* __restrict__ metrics, int64_t* __restrict__ c1) {
   __shared__ __attribute__((aligned(16))) float xs[ROWS][K];
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(THREADS) void lin_train_kernel(
   float4 w[N][KJ];
   load_w_regs(W, w);
   // 2. the step's rows: counter -> (sampler index ->) 16-B image loads, labels
-  const int64_t base = (*ctr) * (int64_t)bfull + row0;
+  const int64_t base = step_row(sr, nrow, *ctr, row0);
   PDM_CHECK(base + nrows <= nrow, "lin_train sample row past the epoch", base, nrow);
   // row -> sample (clamped: a counter driven past the epoch reads a valid row, not a fault)
   auto sample = [&](int r) -> int64_t {
@@ -327,10 +327,10 @@ __global__ __launch_bounds__(256) void lin_eval_kernel(
 }  // namespace
 
 void launch_lin_train(const uint8_t* images, const int32_t* labels, const int32_t* idx,
-                      int64_t nrow, const int64_t* ctr, int bfull, int B, const float* W,
+                      int64_t nrow, const int64_t* ctr, StepRows sr, int B, const float* W,
                       const float* b, float* slab, double* metrics, int64_t* c1, hipStream_t st) {
   const int nblk = (B + ROWS - 1) / ROWS;
-  lin_train_kernel<<<nblk, THREADS, 0, st>>>(images, labels, idx, nrow, ctr, bfull, B, W, b, slab,
+  lin_train_kernel<<<nblk, THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, B, W, b, slab,
                                          metrics, c1);
 }
 

@@ -113,7 +113,7 @@ class CnnStepF32(GpuStepBase):
         ldt = -(-B // 32) * 32
         C.f32_fwd(self.ep_images.view(-1, 784), self.ep_labels, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
-                  self.pool, self.pmask, self.a1g, self.xng, self.ylab)
+                  self.pool, self.pmask, self.a1g, self.xng, self.ylab, spe=self.spe)
         C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN)
         C.cnn_head(self.part, SPLITK_TRAIN, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                    self.ylab, True, None, None, ldt, self.head_slab, self.metrics.train_view(),

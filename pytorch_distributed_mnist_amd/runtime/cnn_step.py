@@ -300,7 +300,7 @@ class CnnStep(GpuStepBase):
         bands = choose_bands(B)
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                  self.pmask, *self.fwd_outputs(B))
+                  self.pmask, *self.fwd_outputs(B), spe=self.spe)
         if carry_in and self.fc_side:
             torch.cuda.current_stream(self.device).wait_event(self._side_ev)
         elif carry_in:

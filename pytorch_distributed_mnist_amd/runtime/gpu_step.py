@@ -55,16 +55,20 @@ class GpuStepBase:
         self.test_labels = prog.test_split.labels.to(device=dev, dtype=torch.int32).contiguous()
         # [train data step, (spare)]
         self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)
-        # the epoch's samples in sampler order, double-buffered (set_train_indices): slot
-        # `self.slot` holds the running epoch, the other one is filled for the next epoch
-        self._ep = [(torch.empty(0, dtype=torch.uint8, device=dev),
-                     torch.empty(0, dtype=torch.int32, device=dev)) for _ in range(2)]
-        self.slot = 0
-        self._pending = None             # (pinned order, slot, event): next epoch's gather
+        # the samples of two consecutive epochs in sampler order (set_train_indices): epoch e
+        # in half e & 1 of the epoch buffer, located by the running data-step counter
+        # (kernels.h StepRows: spe steps per epoch)
+        self.ep_images = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.ep_labels = torch.empty(0, dtype=torch.int32, device=dev)
+        self.spe = 0
+        self._n_epoch = 0
+        self._ctr_host = 0               # the data-step counter's value once the queue drains
+        self._dev_step = None            # the optimizer-step count the device holds (host view)
+        self._pending = None             # [order, half, event | None]: the next epoch's gather
+        self._epoch_start = 0
         self._gather_stream = None       # stream of the ahead-of-time gathers
         self._ring = None                # pinned staging buffers of the epoch orders
         self._ring_i = 0
-        self._step_written = None
         self.use_graphs = bool(use_graphs) and self.reducer.capturable
         self.graphs = {}
         self.bfull = prog.batch_size
@@ -77,13 +81,9 @@ class GpuStepBase:
         self.phase_period = 1
 
     # -- data ----------------------------------------------------------------
-    @property
-    def ep_images(self) -> torch.Tensor:
-        return self._ep[self.slot][0]
-
-    @property
-    def ep_labels(self) -> torch.Tensor:
-        return self._ep[self.slot][1]
+    # workgroups of the ahead-of-time gather that runs beside the steps (0: one per 16 rows);
+    # grid-striding workgroups take fewer CUs for longer
+    AHEAD_GATHER_WGS = int(os.environ.get("PDM_AHEAD_GATHER_WGS", "0"))
 
     def _stage(self, idx: torch.Tensor) -> list:
         """Copy an epoch order into the next pinned staging buffer of a ring of three ([buffer,
@@ -104,74 +104,101 @@ class GpuStepBase:
         buf[0].copy_(idx)
         return buf
 
-    def _gather(self, src: torch.Tensor, slot: int, counters: bool) -> None:
-        n = src.numel()
-        img, lab = self._ep[slot]
-        self.C.gather_epoch(self.train_images, self.train_labels, src, img.view(n, 784), lab,
-                            self.ctr if counters else None,
-                            self.opt._step_dev if counters else None,
-                            int(self.opt.step_count))
+    def _gather(self, idx: torch.Tensor, half: int, stream) -> torch.cuda.Event:
+        """Queue the gather of an epoch order into half `half` of the epoch buffer on `stream`;
+        returns the event behind it."""
+        n = self._n_epoch
+        buf = self._stage(idx)
+        cur_stream = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(stream):
+            self.C.gather_epoch(self.train_images, self.train_labels, buf[0],
+                                self.ep_images.view(-1, 784)[half * n:(half + 1) * n],
+                                self.ep_labels[half * n:(half + 1) * n],
+                                max_wgs=0 if stream is cur_stream else self.AHEAD_GATHER_WGS)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        buf[1] = ev
+        return ev
 
     def set_train_indices(self, idx_cpu: torch.Tensor, next_idx=None) -> None:
         """Install this epoch's sample order; optionally start materialising the next one's.
 
-        ``gather_epoch`` copies the epoch's samples contiguously into an epoch buffer (the
-        step kernels read their rows behind one counter load), reading the order in place
-        from a pinned staging buffer (``EpochIndexPrefetcher`` computes it on its worker
-        thread; only this thread touches pinned memory).  The epoch buffer is double-buffered: with ``next_idx`` given, the next
-        epoch's gather is queued right away on a side stream into the other buffer, behind an
-        event that marks the end of the previous epoch's steps (the last reader of that
-        buffer), so it runs beside this epoch's first steps.  At the next boundary the
-        compute stream then only waits for that event and resets the step counters (one small
-        launch): the boundary costs the GPU almost nothing.  Graphs bake in a buffer address,
-        so they are keyed by the slot too.  The host never waits for queued steps.
+        ``gather_epoch`` copies an epoch's samples contiguously into one half of the epoch
+        buffer (the step kernels read their rows behind one counter load), reading the order
+        in place from a pinned staging buffer (``EpochIndexPrefetcher`` computes it on its
+        worker thread; only this thread touches pinned memory).  The data-step counter is
+        never reset: epoch e = counter / spe lives in half e & 1 (kernels.h StepRows), so the
+        step graphs stay valid across epochs.  With ``next_idx`` given, the next epoch's
+        gather is queued on a side stream into the other half once this epoch is half-way
+        through (``_issue_ahead``), behind an event after the steps queued so far (the other
+        half's last reader, the previous epoch, is among them), and runs beside this epoch's
+        steps.  At the next boundary that gather has long completed (the host checks its
+        event) and the compute stream does not even wait for it: in steady state an epoch
+        boundary enqueues nothing.  The host never waits for queued steps.
         """
         n = idx_cpu.numel()
-        if self._ep[0][0].numel() != n * 784:
-            self._ep = [(torch.empty(n * 784, dtype=torch.uint8, device=self.device),
-                         torch.empty(n, dtype=torch.int32, device=self.device))
-                        for _ in range(2)]
-            self.graphs.clear()          # graphs captured the old buffer addresses
-            self._pending = None
         cur = torch.cuda.current_stream(self.device)
-        p = self._pending
-        self._pending = None
-        if p is not None and p[0] is idx_cpu:
-            # gathered ahead on the side stream: wait for it, reset the counters
-            self.slot = p[1]
-            cur.wait_event(p[2])
-            self.C.gather_epoch(self.train_images, self.train_labels,
-                                torch.empty(0, dtype=torch.int32, device=self.device),
-                                self.ep_images.view(-1, 784), self.ep_labels, self.ctr,
-                                self.opt._step_dev, int(self.opt.step_count))
+        if self._n_epoch != n:
+            self.ep_images = torch.empty(2 * n * 784, dtype=torch.uint8, device=self.device)
+            self.ep_labels = torch.empty(2 * n, dtype=torch.int32, device=self.device)
+            self._n_epoch = n
+            self.spe = -(-n // self.bfull)
+            self.graphs.clear()          # graphs captured the old buffer and geometry
+            self._pending = None
+        # this epoch starts at the next multiple of spe (a partial epoch before it -- tests,
+        # tools -- moves the counter on)
+        start = -(-self._ctr_host // self.spe) * self.spe
+        if start != self._ctr_host:
+            self.ctr[0:1].fill_(start)
+            self._ctr_host = start
+        half = (start // self.spe) & 1
+        p, self._pending = self._pending, None
+        if p is not None and p[0] is idx_cpu and p[1] == half and p[2] is not None:
+            if not p[2].query():         # gathered ahead on the side stream: still running
+                cur.wait_event(p[2])
         else:
-            # first epoch (or the order gathered ahead was not this one): gather in stream
-            # order into the running slot, behind the previous epoch's steps
-            buf = self._stage(idx_cpu)
-            self._gather(buf[0], self.slot, True)
-            buf[1] = torch.cuda.Event()
-            buf[1].record(cur)
-        self._step_written = self.opt.step_count
+            if p is not None and p[2] is not None:
+                cur.wait_event(p[2])     # an unused ahead gather still writes a half
+            self._gather(idx_cpu, half, cur)
+        self._epoch_start = start
         if next_idx is not None and next_idx.numel() == n:
             if self._gather_stream is None:
+                # created and used once here, not inside a timed run: HIP sets up a stream's
+                # hardware queue at its first launch (~5 ms of host time)
                 self._gather_stream = torch.cuda.Stream(self.device)
-            free = torch.cuda.Event()
-            free.record(cur)             # everything queued so far: the previous epoch's steps
-            buf = self._stage(next_idx)
-            other = 1 - self.slot
-            with torch.cuda.stream(self._gather_stream):
-                self._gather_stream.wait_event(free)
-                self._gather(buf[0], other, False)
-                done = torch.cuda.Event()
-                done.record(self._gather_stream)
-            buf[1] = done
-            self._pending = (next_idx, other, done)
+                with torch.cuda.stream(self._gather_stream):
+                    torch.zeros(1, device=self.device)
+            self._pending = [next_idx, 1 - half, None]
+
+    def _issue_ahead(self) -> None:
+        """Queue the next epoch's gather on the side stream once this epoch is half-way
+        through (train_steps calls this between replays): the copy then runs beside steps in
+        the middle of an epoch rather than beside the first steps after a boundary."""
+        p = self._pending
+        if p is None or p[2] is not None or \
+                self._ctr_host - self._epoch_start < max(1, self.spe // 2):
+            return
+        # the side stream waits for everything queued on the compute stream so far (an event
+        # recorded now: waiting on one recorded at the boundary, before the graph replays,
+        # cost the host ~5 ms in hipStreamWaitEvent); the other half's last reader, the
+        # previous epoch, is among it
+        free = torch.cuda.Event()
+        free.record(torch.cuda.current_stream(self.device))
+        self._gather_stream.wait_event(free)
+        p[2] = self._gather(p[0], p[1], self._gather_stream)
+
+    def skip_steps(self, k: int) -> None:
+        """Move the data-step counter k steps on within the epoch (bench.py positions its
+        timed window; every step is the same kernel chain on a different batch)."""
+        self.ctr[0:1].add_(k)
+        self._ctr_host += k
+        self._issue_ahead()              # as the skipped steps would have
 
     def begin_epoch(self) -> None:
         self.opt.sync_hyperparams()
-        if self._step_written != self.opt.step_count:
+        if self._dev_step != self.opt.step_count:
             self.opt.sync_step()
-        self._step_written = None
+            self._dev_step = self.opt.step_count
 
     # -- step ------------------------------------------------------------------
     # One hipGraph replay costs ~10-16 us of host time (MI355X_MICROARCH.md price
@@ -184,7 +211,7 @@ class GpuStepBase:
 
     def _graph(self, B: int, nsteps: int, phase=None):
         phase = self.phase if phase is None else phase
-        key = (B, nsteps, phase, self.slot)
+        key = (B, nsteps, phase)
         g = self.graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
@@ -204,20 +231,12 @@ class GpuStepBase:
 
     def prepare(self, B: int) -> None:
         """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, both
-        step phases, both epoch buffers), so no capture or first-launch upload lands inside a
-        timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
+        step phases), so no capture or first-launch upload lands inside a timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
         when replayed."""
         if not self.use_graphs:
             return
-        saved = self.slot
-        todo = [(n, ph, sl) for n in self.GRAPH_SIZES for ph in range(self.phase_period)
-                for sl in range(2)]
-        for n, ph, sl in todo:
-            self.slot = sl
-            try:
-                g = self._graph(B, n, ph)
-            finally:
-                self.slot = saved
+        for n, ph in ((n, ph) for n in self.GRAPH_SIZES for ph in range(self.phase_period)):
+            g = self._graph(B, n, ph)
             try:
                 exe = g.raw_cuda_graph_exec()
             except (AttributeError, RuntimeError):
@@ -233,15 +252,19 @@ class GpuStepBase:
             return
         if self.use_graphs:
             k = self.GRAPH_STEPS
-            for _ in range(n // k):
-                self._replay(B, k)
             r = n % k
-            for size in self.GRAPH_SIZES[1:]:
-                if r & size:
-                    self._replay(B, size)
+            for size in [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]:
+                self._issue_ahead()
+                self._replay(B, size)
+                self._ctr_host += size
         else:
+            self._issue_ahead()
             self._train_seq(B, n)
+            self._ctr_host += n
+        self._issue_ahead()
         self.opt.step_count += n
+        if self._dev_step is not None:
+            self._dev_step += n
 
     def train_step(self, B: int) -> None:
         self.train_steps(B, 1)
@@ -350,7 +373,8 @@ class LinearStep(GpuStepBase):
     def _train_impl(self, B: int) -> None:
         C = self.C
         C.lin_train(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull,
-                    B, self.W, self.b, self.slab, self.metrics.train_view(), self.opt._step_dev)
+                    B, self.W, self.b, self.slab, self.metrics.train_view(), self.opt._step_dev,
+                    spe=self.spe)
         red = self.reducer
         # the step's train loss / correct partials sit in the slabs (columns 7850, 7851): the
         # launch that sums the gradient slabs adds them to the fp64 metrics in a fixed order

@@ -1,13 +1,16 @@
-# Epoch-boundary check: the data-path GPU tests, the boundary probe, the driver-length bench
-# (--steps 20 --warmup 5) with its host timeline, and the default-length bench.
+# Driver-length bench (--steps 20 --warmup 5): epoch boundary variants, interleaved.
 set -o pipefail
 mkdir -p gpurun_out
 L=gpurun_out/short.log
 : > $L
-timeout -k 10 400 python -u -m pytest tests/test_gpu_cnn.py tests/test_gpu_linear.py tests/test_gpu_app.py tests/test_gpu_cnn_f32.py -x -q --timeout 120 --timeout-method thread >> $L 2>&1 || exit 1
-timeout -k 10 120 python tools/boundary_probe.py >> $L 2>&1 || exit 1
-for i in 1 2 3; do
-  PDM_BENCH_DEBUG=1 timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 >> $L 2>&1 || exit 1
+for i in 1 2; do
+  for e in "X=1" "PDM_BENCH_BOUNDARY=0" "PDM_GATHER_AHEAD=0"; do
+    echo "== $e" >> $L
+    env $e timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 >> $L 2>&1 || exit 1
+  done
 done
-PDM_BENCH_DEBUG=1 timeout -k 10 120 python bench.py --gpus 1 --steps 200 --warmup 30 >> $L 2>&1 || exit 1
+echo "== 200 steps" >> $L
+timeout -k 10 120 python bench.py --gpus 1 --steps 200 --warmup 30 >> $L 2>&1 || exit 1
+echo "== 470 steps" >> $L
+timeout -k 10 120 python bench.py --gpus 1 --steps 470 --warmup 30 >> $L 2>&1 || exit 1
 echo done >> $L
