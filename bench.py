@@ -275,21 +275,22 @@ def main():
         # capture + upload the step graphs outside the timed window (a graph captured lazily
         # on first use would put its capture inside a short timed run)
         prog.gpu.prepare(B)
-        run(a.warmup)
         # put the next epoch boundary inside the timed window: continue the current epoch
-        # from the step that leaves K // 2 full steps before the boundary (every step is the
-        # same kernel chain on a different batch of the sampler order)
+        # from the step that leaves W warmup steps and then K // 2 timed full steps before
+        # the boundary (every step is the same kernel chain on a different batch of the
+        # sampler order).  The counter moves first, so the skipped part of the epoch also
+        # issues what it would have issued (the next epoch's gather, from mid-epoch), and
+        # the W warmup steps run right before the timed window as usual.
         left = full - state["step"]
-        if a.steps >= 2 and left > a.steps // 2 and os.environ.get("PDM_BENCH_BOUNDARY", "1") != "0":
-            skip = left - a.steps // 2
+        if a.steps >= 2 and left > a.steps // 2 + a.warmup and \
+                os.environ.get("PDM_BENCH_BOUNDARY", "1") != "0":
+            skip = left - a.steps // 2 - a.warmup
             sync("reposition")
             prog.gpu.skip_steps(skip)          # device data-step counter
             state["step"] += skip
+        run(a.warmup)
         left = full - state["step"]
         boundaries = -(-(a.steps - left) // full) if a.steps > left else 0
-        if os.environ.get("PDM_BENCH_PRECOMPUTE") == "1":   # diagnostic: no sampler work in the window
-            for e in range(state["epoch"], state["epoch"] + 4):
-                prefetch.peek(e)
         elapsed = timed(a.steps)
         chosen.check()
         if not torch.isfinite(arena.params).all():
