@@ -29,11 +29,14 @@ st = p.gpu
 st.begin_epoch()
 st.prepare(B)
 done = 0
+epoch = 0
 
 
 def window(k):
-    global done
-    if done + k > 230:                  # stay inside one epoch (234 full steps)
+    global done, epoch
+    if done + k > 230:                  # stay inside one epoch (234 full steps): start the next
+        epoch += 1                      # (the counter runs on; the ragged tail step is skipped)
+        p.set_train_indices(distributed_indices(len(train), 1, 0, epoch))
         st.begin_epoch()
         done = 0
     torch.cuda.synchronize()
