@@ -71,22 +71,26 @@ def test_linear_cli_gpu_matches_cpu(gpu, tmp_path):
 def test_two_ranks_on_one_gpu_match_one_rank(gpu, tmp_path, monkeypatch):
     """The multi-rank GPU program (world_size 2: bucket all-reduces, 1/ws scaling, unfused
     conv reduction, sharded sampler) rehearsed on one GPU with a gloo data plane
-    (PDM_SHARE_DEVICE; RCCL itself refuses two ranks on one device).  After one epoch the
-    weights match the world_size-1 run to bf16 accuracy (same global batches)."""
+    (PDM_SHARE_DEVICE; RCCL itself refuses two ranks on one device).  After each of two
+    epochs (the second crosses an epoch boundary of the running data-step counter, with the
+    next epoch gathered ahead on every rank) the weights match the world_size-1 run to bf16
+    accuracy (same global batches)."""
     monkeypatch.setenv("PDM_SHARE_DEVICE", "1")
     d1, d2 = tmp_path / "ws1", tmp_path / "ws2"
     d1.mkdir()
     d2.mkdir()
     common = ["--arch", "cnn", "--optimizer", "sgd", "--lr", "0.05", "--synthetic-size", "2048",
-              "--epochs", "1", "--seed", "9"]
+              "--epochs", "2", "--seed", "9"]
     cli(common + ["--world-size", "1"], d1, backend="gloo")
     out = cli(common + ["--world-size", "2"], d2, backend="gloo")
-    assert sum(1 for l in out if EPOCH_RE.match(l)) == 2
-    a = torch.load(d1 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)["state_dict"]
-    b = torch.load(d2 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)["state_dict"]
-    for k in a:
-        err = ((a[k] - b[k]).norm() / a[k].norm()).item()
-        assert err < 2e-2, (k, err)
+    assert sum(1 for l in out if EPOCH_RE.match(l)) == 4
+    for ep in (0, 1):
+        name = f"checkpoint_{ep}.pth.tar"
+        a = torch.load(d1 / "checkpoints" / name, weights_only=True)["state_dict"]
+        b = torch.load(d2 / "checkpoints" / name, weights_only=True)["state_dict"]
+        for k in a:
+            err = ((a[k] - b[k]).norm() / a[k].norm()).item()
+            assert err < 2e-2, (ep, k, err)
 
 
 def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path):
