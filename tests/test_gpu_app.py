@@ -88,9 +88,13 @@ def test_two_ranks_on_one_gpu_match_one_rank(gpu, tmp_path, monkeypatch):
         name = f"checkpoint_{ep}.pth.tar"
         a = torch.load(d1 / "checkpoints" / name, weights_only=True)["state_dict"]
         b = torch.load(d2 / "checkpoints" / name, weights_only=True)["state_dict"]
+        # bf16 partial sums reduced in a different order drift apart with SGD momentum: 2 %
+        # after 8 steps, 5 % after 16 (the other epoch's or another rank's samples would put
+        # every tensor far off)
+        tol = 2e-2 if ep == 0 else 5e-2
         for k in a:
             err = ((a[k] - b[k]).norm() / a[k].norm()).item()
-            assert err < 2e-2, (ep, k, err)
+            assert err < tol, (ep, k, err)
 
 
 def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path):
