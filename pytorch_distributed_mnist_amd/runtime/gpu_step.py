@@ -178,10 +178,8 @@ class GpuStepBase:
         if p is None or p[2] is not None or \
                 self._ctr_host - self._epoch_start < max(1, self.spe // 2):
             return
-        # the side stream waits for everything queued on the compute stream so far (an event
-        # recorded now: waiting on one recorded at the boundary, before the graph replays,
-        # cost the host ~5 ms in hipStreamWaitEvent); the other half's last reader, the
-        # previous epoch, is among it
+        # the side stream waits for everything queued on the compute stream so far; the other
+        # half's last reader, the previous epoch, is among it
         free = torch.cuda.Event()
         free.record(torch.cuda.current_stream(self.device))
         self._gather_stream.wait_event(free)
