@@ -24,6 +24,9 @@ import torch
 from ..ops import _ext
 
 
+_GRAPH_STEPS = int(os.environ.get("PDM_GRAPH_STEPS", "8"))   # steps per graph: a power of two
+
+
 def make_gpu_step(prog, use_graphs: bool = True):
     if prog.model == "linear":
         if prog.dtype != "fp32":
@@ -204,8 +207,8 @@ class GpuStepBase:
     # steps are captured GRAPH_STEPS at a time (identical steps: the batch comes
     # from the device counter) and a run of n steps replays n // GRAPH_STEPS
     # multi-step graphs plus one graph per set bit of the remainder (4, 2, 1 steps).
-    GRAPH_STEPS = 8
-    GRAPH_SIZES = (8, 4, 2, 1)
+    GRAPH_STEPS = _GRAPH_STEPS
+    GRAPH_SIZES = tuple(_GRAPH_STEPS >> i for i in range(_GRAPH_STEPS.bit_length()))
 
     def _graph(self, B: int, nsteps: int, phase=None):
         phase = self.phase if phase is None else phase
