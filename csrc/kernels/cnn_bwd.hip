@@ -59,7 +59,16 @@ using namespace cnn;
 #else
 #define FC_STAMP(row, slot) do { } while (0)
 #endif
-constexpr int DW_TILES = FEAT / 64;  // 144
+// dW tile: 64 feature columns x 64 * DW_MT hidden rows (each of the 4 waves owns DW_MT 16-row
+// m-tiles).  DW_MT = 1 splits the 128 hidden rows over two workgroups (288 tiles): half the
+// MFMA work and half the fused update's epilogue per workgroup, twice the workgroups.
+#ifndef PDM_DW_MT
+#define PDM_DW_MT 1
+#endif
+constexpr int DW_MT = PDM_DW_MT;
+static_assert(DW_MT == 1 || DW_MT == 2, "dW tile: 64 or 128 hidden rows");
+constexpr int DW_FT = FEAT / 64;                      // 144 feature tiles
+constexpr int DW_TILES = DW_FT * (2 / DW_MT);         // 144 or 288
 constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
 constexpr int DX_COLS = 384;         // dX tile: 32 batch rows x 384 features per workgroup
 constexpr int DX_TILES = FEAT / DX_COLS;   // 24 = 8 XCDs x 3
@@ -91,20 +100,22 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   const int bid = blockIdx.x + bid_offset;
 
   if (bid < DW_TILES) {
-    // ---- dW1 tile: all 128 hidden rows x 64 feature columns, K = batch ----
+    // ---- dW1 tile: 64 * DW_MT hidden rows (from n0) x 64 feature columns, K = batch ----
     // The batch is consumed in chunks of DWC rows: the whole chunk (pool rows and the
     // dh^T A fragments) is loaded with every load in flight at once, and the next chunk's
-    // loads are issued before the current chunk's MFMAs.
-    const int k0 = bid * 64;
+    // loads are issued before the current chunk's MFMAs.  The two hidden halves of a
+    // feature tile (DW_MT = 1) are DW_FT workgroups apart: the same XCD, one L2 copy of the
+    // pool tile they both read.
+    const int k0 = (bid % DW_FT) * 64, n0 = (bid / DW_FT) * 64 * DW_MT;
     FC_STAMP(bid, 8);
-    f32x4 acc[2][4];
+    f32x4 acc[DW_MT][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < DW_MT; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int srow = tid >> 3, sch = tid & 7;
     uint4 pv[DWC / 32];
-    bf16x8 a[2][DWC / 32];
+    bf16x8 a[DW_MT][DWC / 32];
     auto load_chunk = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < DWC / 32; ++j) {
@@ -116,25 +127,26 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         pv[j] = row < B ? v : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < DW_MT; ++mt)
 #pragma unroll
         for (int kk = 0; kk < DWC / 32; ++kk)
           a[mt][kk] = *reinterpret_cast<const bf16x8*>(   // fragment-major dh^T (frag_pos)
-              dht + ((int64_t)((wave * 2 + mt) * (ldt / 32) + (min(c0 + 32 * kk, ldt - 32) >> 5)) * 64 +
-                     lane) * 8);
+              dht + ((int64_t)((n0 / 16 + wave * DW_MT + mt) * (ldt / 32) +
+                               (min(c0 + 32 * kk, ldt - 32) >> 5)) * 64 + lane) * 8);
     };
     load_chunk(0);
     // fused update (fcu.kind >= 0): this tile's fp32 weights and momentum, issued behind the
     // first chunk so they have landed by the epilogue
-    float fpv[2][4][4], fmv[2][4][4];
+    float fpv[DW_MT][4][4], fmv[DW_MT][4][4];
     if (fcu.kind >= 0) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < DW_MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
-            const int64_t q = (int64_t)(wave * 32 + mt * 16 + 4 * g + r) * FEAT + k0 + 16 * nt + i16;
+            const int64_t q = (int64_t)(n0 + wave * 16 * DW_MT + mt * 16 + 4 * g + r) * FEAT + k0 +
+                              16 * nt + i16;
             fpv[mt][r][nt] = fcu.p[q];
             fmv[mt][r][nt] = fcu.m[q];
           }
@@ -144,9 +156,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < DWC / 32; ++j)
         *reinterpret_cast<uint4*>(tile + tile_off(srow + 32 * j, sch * 16)) = pv[j];
-      bf16x8 ac[2][DWC / 32];
+      bf16x8 ac[DW_MT][DWC / 32];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < DW_MT; ++mt)
 #pragma unroll
         for (int kk = 0; kk < DWC / 32; ++kk) ac[mt][kk] = a[mt][kk];
       __syncthreads();
@@ -163,7 +175,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
             const s16x4 hi = lds_tr16(tile + tile_off(32 * kk + 8 * g + 4 + q, 32 * nt + 8 * pq));
             const bf16x8 bv = cat_tr(lo, hi);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < DW_MT; ++mt)
               acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ac[mt][kk], bv, acc[mt][nt], 0, 0, 0);
           }
         }
@@ -172,10 +184,10 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     FC_STAMP(bid, 11);
     if (fcu.kind < 0 || fcu.store_grad) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < DW_MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int n = wave * 32 + mt * 16 + 4 * g + r;
+          const int n = n0 + wave * 16 * DW_MT + mt * 16 + 4 * g + r;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + 16 * nt + i16] = acc[mt][nt][r];
         }
@@ -188,46 +200,56 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       using namespace optim_detail;
       const Hyper h = make_hyper<OPT_SGD>(fcu);
       // the bf16 copy is fragment-major (fc1_fwd's B operand, kernels.h frag_pos): this tile
-      // is 8 n-tiles x 2 k-steps of 1-KB blocks, assembled in LDS and stored as 16-B chunks
+      // is 4 DW_MT n-tiles x 2 k-steps of 1-KB blocks, assembled in LDS and stored as 16-B
+      // chunks
       __syncthreads();   // every wave's last reads of the pool tile are done
       bf16* fr = reinterpret_cast<bf16*>(tile);
-      // W1^T fragments of this tile (kernels.h shadow_t_pos, m = feature): 4 n-tiles x 4
-      // 16-feature blocks of 1 KB, one contiguous 16 KB range; a lane's 4 rows r are 4
-      // consecutive bf16 (one 8-B store, 512 B contiguous per wave store)
+      // W1^T fragments of this tile (kernels.h shadow_t_pos, m = feature, k = hidden): for
+      // each of the 4 16-feature m-frags, the 2 DW_MT 32-row k-frags of this tile, 1 KB each
+      // (one contiguous range per m-frag); a lane's 4 rows r are 4 consecutive bf16 (one 8-B
+      // store, 512 B contiguous per wave store)
       bf16* frt = reinterpret_cast<bf16*>(tile + DWC * 128);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < DW_MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           bf16 pt[4];
+          const int nl0 = wave * 16 * DW_MT + mt * 16 + 4 * g;   // tile-local row of r = 0
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int n = wave * 32 + mt * 16 + 4 * g + r, kl = 16 * nt + i16;
-            const int64_t q = (int64_t)n * FEAT + k0 + kl;
+            const int nl = nl0 + r, kl = 16 * nt + i16;
+            const int64_t q = (int64_t)(n0 + nl) * FEAT + k0 + kl;
             float m = fmv[mt][r][nt], v = 0.f;
             const float p = update<OPT_SGD>(fpv[mt][r][nt], acc[mt][nt][r], m, v, h, fcu.grad_scale);
             fcu.p[q] = p;
             fcu.m[q] = m;
             pt[r] = to_bf16(p);
-            fr[(((n >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (n & 15)) * 8 + (kl & 7)] = pt[r];
+            fr[(((nl >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (nl & 15)) * 8 + (kl & 7)] = pt[r];
           }
           if (fcu.shadow_t_next != nullptr)
-            *reinterpret_cast<bf16x4*>(frt + (((nt * 4 + wave) * 64 + (mt * 2 + (g >> 1)) * 16 + i16) * 8 +
+            *reinterpret_cast<bf16x4*>(frt + (((nt * (2 * DW_MT) + (nl0 >> 5)) * 64 +
+                                               (((nl0 >> 4) & 1) * 2 + (g >> 1)) * 16 + i16) * 8 +
                                               (g & 1) * 4)) = bf16x4{pt[0], pt[1], pt[2], pt[3]};
         }
       __syncthreads();
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = tid + 256 * u, blk = c >> 6;   // blk = n-tile * 2 + k-step
-        *reinterpret_cast<uint4*>(fcu.shadow + ((int64_t)((blk >> 1) * (FEAT / 32) + (k0 >> 5) +
-                                                          (blk & 1)) * 64 + (c & 63)) * 8) =
+      for (int u = 0; u < 2 * DW_MT; ++u) {
+        const int c = tid + 256 * u, blk = c >> 6;   // blk = local n-tile * 2 + k-step
+        *reinterpret_cast<uint4*>(fcu.shadow + ((int64_t)((n0 / 16 + (blk >> 1)) * (FEAT / 32) +
+                                                          (k0 >> 5) + (blk & 1)) * 64 + (c & 63)) * 8) =
             reinterpret_cast<const uint4*>(fr)[c];
       }
       if (fcu.shadow_t_next != nullptr) {
-        bf16* wt_next = fcu.shadow_t_next + (int64_t)k0 * HID;
+        // local block lb = m-frag * 2 DW_MT + local k-frag -> global block
+        // (k0 / 16 + m-frag) * (HID / 32) + n0 / 32 + local k-frag, 64 uint4 each
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          reinterpret_cast<uint4*>(wt_next)[tid + 256 * u] = reinterpret_cast<const uint4*>(frt)[tid + 256 * u];
+        for (int u = 0; u < 2 * DW_MT; ++u) {
+          const int c = tid + 256 * u, lb = c >> 6;
+          const int64_t gb = (int64_t)(k0 / 16 + lb / (2 * DW_MT)) * (HID / 32) + n0 / 32 +
+                             lb % (2 * DW_MT);
+          reinterpret_cast<uint4*>(fcu.shadow_t_next)[gb * 64 + (c & 63)] =
+              reinterpret_cast<const uint4*>(frt)[c];
+        }
       }
     }
     FC_STAMP(bid, 13);
