@@ -43,7 +43,7 @@ REFERENCE_LINEAR_IMG_S_1GPU = 221060.4
 NODE_BATCH = 256          # reference --batch-size default (node total, S:297-300)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -61,18 +61,105 @@ def parse():
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--timeout", type=float, default=600.0,
                     help="deadline (s) for RCCL init and every host sync")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + rendezvous only (gloo, CPU): each rank joins the process "
+                         "group, all-reduces its rank and rank 0 prints one JSON line; tests the "
+                         "self-spawn path without a GPU")
+    return ap.parse_args(argv)
+
+
+def launch_mode(gpus: int, env) -> str:
+    """How this process runs: 'worker' (one rank of a launched job: torch.distributed.run or
+    our own spawn set RANK / WORLD_SIZE), 'spawn' (--gpus N > 1 from a plain ``python`` call:
+    start the N rank processes, as the reference's default entry does with mp.spawn,
+    multi_proc_single_gpu.py:284-285, :359) or 'single' (N = 1, no launcher)."""
+    if "WORLD_SIZE" in env:
+        ws = int(env["WORLD_SIZE"])
+        if ws != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}")
+        return "worker" if ws > 1 else "single"
+    return "spawn" if gpus > 1 else "single"
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start N rank processes of this script with the env:// rendezvous variables
+    torch.distributed.run would set (127.0.0.1, a free port; RANK = LOCAL_RANK = i).  This
+    process has not touched the GPU (only ``import torch``), so starting children is safe.
+    The children inherit stdout / stderr: rank 0 prints the one JSON line.  If any rank
+    fails, the others are terminated (by PID) and its exit status is returned."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=port, PDM_BENCH_SPAWNED="1")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                          env=env))
+        rc = 0
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+
+
+def dry_run(a, rank: int, ws: int) -> None:
+    import torch.distributed as dist
+    if os.environ.get("PDM_BENCH_FAIL_RANK") == str(rank):
+        sys.exit(3)                 # fault injection (tests): this rank dies before rendezvous
+    if ws > 1:
+        dist.init_process_group("gloo", init_method="env://", world_size=ws, rank=rank)
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        total = float(t.item())
+        dist.destroy_process_group()
+    else:
+        total = 0.0
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": ws, "rank_sum": total,
+                          "launch": "spawned" if os.environ.get("PDM_BENCH_SPAWNED") else
+                          ("launcher" if ws > 1 else "single")}), flush=True)
 
 
 def main():
     a = parse()
+    mode = launch_mode(a.gpus, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws != a.gpus and ws == 1 and a.gpus > 1:
-        print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} procs",
-              file=sys.stderr)
-        sys.exit(2)
+    if a.dry_run:
+        dry_run(a, rank, ws)
+        return
     from types import SimpleNamespace
 
     from pytorch_distributed_mnist_amd import parallel
@@ -149,19 +236,21 @@ def main():
     def measure(B: int) -> dict:
         """Calibrate the transport for per-rank batch B, then time a.steps steps."""
         prog = TrainProgram(model, dtype, arena, opt, first, train, test, B, use_graphs=a.graphs)
-        full = -(-n // ws) // B                    # full-batch steps per epoch
+        # the reference's epoch (DataLoader drop_last=False, S:152-157): the rank's padded
+        # DistributedSampler share in full batches, then one ragged tail batch
+        full, tail = divmod(-(-n // ws), B)
+        spe = full + (1 if tail else 0)            # steps per epoch
         state = {"epoch": 0, "step": 0}
 
-        cut = {}
+        orders = {}
 
         def order(e):
-            """Epoch e's order, full batches only: the bench times full steps, so its epochs
-            are the sampler order without the ragged tail (one object per epoch: the program
-            recognises the order it gathered ahead by identity)."""
-            if e not in cut:
-                cut[e] = prefetch.peek(e)[:full * B]
-                cut.pop(e - 3, None)
-            return cut[e]
+            """Epoch e's sampler order (one object per epoch: the program recognises the order
+            it gathered ahead by identity)."""
+            if e not in orders:
+                orders[e] = prefetch.peek(e)
+                orders.pop(e - 3, None)
+            return orders[e]
 
         dbg = os.environ.get("PDM_BENCH_DEBUG")
         marks = []
@@ -185,14 +274,24 @@ def main():
             state["step"] = 0
 
         def run(k):
+            """Enqueue k steps of the epoch sequence; returns the images they train on."""
+            imgs = 0
             while k > 0:
-                if state["step"] >= full:
+                if state["step"] >= spe:
                     next_epoch()
-                m = min(k, full - state["step"])
-                mark(f"replay {m}")
-                prog.gpu.train_steps(B, m)
+                if state["step"] < full:
+                    m = min(k, full - state["step"])
+                    mark(f"replay {m}")
+                    prog.gpu.train_steps(B, m)
+                    imgs += m * B
+                else:                              # the epoch's ragged tail step
+                    m = 1
+                    mark(f"tail {tail}")
+                    prog.gpu.train_steps(tail, 1)
+                    imgs += tail
                 state["step"] += m
                 k -= m
+            return imgs
 
         def timed(k):
             sync("warmup")
@@ -200,7 +299,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             marks.clear()
-            run(k)
+            imgs = run(k)
             mark("sync")
             sync("timed steps")
             mark("end")
@@ -210,16 +309,24 @@ def main():
                       flush=True)
             barrier()
             torch.cuda.synchronize()
-            return allmax(time.perf_counter() - t0)
+            return allmax(time.perf_counter() - t0), imgs
 
         def use(red, carry="carry"):
             prog.reducer = red
             prog.gpu.reducer = red
             prog.gpu.use_graphs = bool(a.graphs) and red.capturable
             if hasattr(prog.gpu, "fc_carry"):
-                prog.gpu.fc_carry = carry != "nocarry"
+                prog.gpu.fc_carry = carry not in ("nocarry", "early")
                 prog.gpu.fc_side = carry == "side"
+                prog.gpu.fc_early = carry == "early"
             prog.gpu.invalidate_graphs()
+
+        def prepare():
+            """Capture + upload the step graphs outside any timed window (a graph captured
+            lazily on first use would put its capture inside a short timed run)."""
+            prog.gpu.prepare(B)
+            if tail:
+                prog.gpu.prepare(tail, sizes=(1,))
 
         # candidate step structures: every transport, and for RCCL the fc-update placement
         # (cnn_step.CnnStep.fc_carry / fc_side: carried past the next cnn_fwd, one grouped
@@ -228,7 +335,7 @@ def main():
         for name, red in reducers.items():
             if name == "rccl" and model == "cnn" and os.environ.get("PDM_FC_CARRY") is None:
                 cands += [("rccl", red, "carry"), ("rccl-nocarry", red, "nocarry"),
-                          ("rccl-side", red, "side")]
+                          ("rccl-side", red, "side"), ("rccl-early", red, "early")]
             else:
                 env = os.environ.get("PDM_FC_CARRY", "1") != "0"
                 side = os.environ.get("PDM_FC_SIDE", "0") == "1"
@@ -240,9 +347,9 @@ def main():
         if len(cands) > 1:
             for name, red, carry in cands:
                 use(red, carry)
-                prog.gpu.prepare(B)            # capture outside the calibration window
+                prepare()                      # capture outside the calibration window
                 run(16)
-                calib[name] = timed(48) / 48 * 1e3
+                calib[name] = timed(48)[0] / 48 * 1e3
                 try:
                     red.check()
                     ok = 1
@@ -272,16 +379,14 @@ def main():
             use(cands[0][1], cands[0][2])
             best = cands[0][0]
         chosen = prog.reducer
-        # capture + upload the step graphs outside the timed window (a graph captured lazily
-        # on first use would put its capture inside a short timed run)
-        prog.gpu.prepare(B)
+        prepare()
         # put the next epoch boundary inside the timed window: continue the current epoch
         # from the step that leaves W warmup steps and then K // 2 timed full steps before
         # the boundary (every step is the same kernel chain on a different batch of the
         # sampler order).  The counter moves first, so the skipped part of the epoch also
         # issues what it would have issued (the next epoch's gather, from mid-epoch), and
         # the W warmup steps run right before the timed window as usual.
-        left = full - state["step"]
+        left = spe - state["step"]
         if a.steps >= 2 and left > a.steps // 2 + a.warmup and \
                 os.environ.get("PDM_BENCH_BOUNDARY", "1") != "0":
             skip = left - a.steps // 2 - a.warmup
@@ -289,15 +394,16 @@ def main():
             prog.gpu.skip_steps(skip)          # device data-step counter
             state["step"] += skip
         run(a.warmup)
-        left = full - state["step"]
-        boundaries = -(-(a.steps - left) // full) if a.steps > left else 0
-        elapsed = timed(a.steps)
+        left = spe - state["step"]
+        boundaries = -(-(a.steps - left) // spe) if a.steps > left else 0
+        elapsed, imgs = timed(a.steps)
         chosen.check()
         if not torch.isfinite(arena.params).all():
             raise RuntimeError("non-finite parameters after the benchmark")
         ms = elapsed / a.steps * 1e3
         return {"B": B, "global_batch": B * ws, "elapsed": elapsed, "ms": ms,
-                "value": a.steps * B * ws / elapsed, "transport": best,
+                "value": imgs * ws / elapsed, "images": imgs * ws, "tail": tail,
+                "epoch_steps": spe, "transport": best,
                 "calib": {k: round(v, 5) for k, v in calib.items()},
                 "graphs": bool(prog.gpu.use_graphs), "epoch_boundaries_timed": boundaries}
 
@@ -338,8 +444,21 @@ def main():
                        "seq_len": None, "parallelism": f"dp{ws}", "optimizer": optname,
                        "graphs": m["graphs"], "grad_transport": m["transport"],
                        "transport_calibration_ms_per_step": m["calib"],
-                       "epoch_boundaries_timed": m["epoch_boundaries_timed"]},
+                       "epoch_boundaries_timed": m["epoch_boundaries_timed"],
+                       "epoch_steps": m["epoch_steps"], "tail_batch_per_rank": m["tail"],
+                       "images_timed": m["images"]},
+            "value_semantics": (
+                "weak scaling: images/sec of the whole node at a fixed per-rank batch; timed "
+                "window = K consecutive steps of the reference's epoch sequence (full batches "
+                "+ the ragged tail, an epoch boundary inside); value = images_timed / time"
+                if main_mode == "weak" else
+                "strong scaling: the reference's node batch 256 split over the ranks (S:174)"),
             "comm": comm_info,
+            # every PDM_* environment knob this run saw (none set = the defaults)
+            "knobs": {k: v for k, v in sorted(os.environ.items())
+                      if k.startswith("PDM_") and k != "PDM_BENCH_SPAWNED"},
+            "launch": "spawned" if os.environ.get("PDM_BENCH_SPAWNED") else
+                      ("launcher" if ws > 1 else "single"),
         }
         if main_mode == "weak" and "strong" in res:
             s = res["strong"]
@@ -348,6 +467,7 @@ def main():
                               "grad_transport": s["transport"],
                               "transport_calibration_ms_per_step": s["calib"],
                               "epoch_boundaries_timed": s["epoch_boundaries_timed"],
+                              "tail_batch_per_rank": s["tail"], "images_timed": s["images"],
                               "semantics": "reference DDP: node batch 256 split over ranks (S:174)"}
         print(json.dumps(line), flush=True)
     prefetch.close()

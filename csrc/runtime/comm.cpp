@@ -113,7 +113,16 @@ class RcclComm {
   void destroy() {
     if (comm_) {
       hipStreamSynchronize(stream_);
-      ncclCommDestroy(comm_);
+      // non-blocking communicator: finalize (flushes outstanding operations, in progress
+      // until every peer has done the same) is polled against the deadline; a peer that
+      // never finalizes gets the communicator aborted instead of a hang in destroy
+      ncclResult_t r = ncclCommFinalize(comm_);
+      if (r == ncclInProgress || r == ncclSuccess) r = settle("communicator finalize");
+      if (r == ncclSuccess) {
+        ncclCommDestroy(comm_);
+      } else {
+        ncclCommAbort(comm_);
+      }
       comm_ = nullptr;
       release_stream();
     }

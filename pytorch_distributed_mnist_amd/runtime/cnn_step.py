@@ -187,9 +187,16 @@ class CnnStep(GpuStepBase):
         # waits for it.  Worth it when those kernels leave CUs idle (small per-rank batches:
         # cnn_fwd_band is 192 workgroups at B = 32 / 64); bench.py calibrates it as well.
         self.fc_side = os.environ.get("PDM_FC_SIDE", "0") == "1"
+        # ... or (fc_early) issue the fc bucket's all-reduce right after fc1_bwd, so it runs
+        # during the conv backward, as DDP's Reducer does during loss.backward()
+        # (multi_proc_single_gpu.py:91).  At small per-rank batches cnn_bwd_band leaves CUs
+        # free for RCCL's kernel (B = 32: 192 workgroups on 256 CUs); at B = 256 cnn_bwd takes
+        # every CU and the collective waits for it.  bench.py calibrates it as well.
+        self.fc_early = os.environ.get("PDM_FC_EARLY", "0") == "1"
         self._side = None
         self._side_ev = None
         self.refresh_shadows()
+        self._poison_unkept_grads()
 
     @torch.no_grad()
     def refresh_shadows(self) -> None:
@@ -275,7 +282,7 @@ class CnnStep(GpuStepBase):
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
         carry = (self.reducer.active and getattr(self.reducer, "kind", None) == "rccl" and
-                 self.fc_carry)
+                 self.fc_carry and not self.fc_early)
         streamed = self.reducer.streamed
         if streamed:
             self.reducer.begin(n)        # one persistent xgmi collective for the n steps
@@ -315,7 +322,13 @@ class CnnStep(GpuStepBase):
                   self.metrics.train_view(),
                   self._fc_update() if self.fuse_fc1 and self.fuse_conv_reduce else None)
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
+        rccl_early = (self.fc_early and not xgmi and red.active and
+                      getattr(red, "_native", None) is not None)
         early = xgmi and not red.streamed and os.environ.get("PDM_XGMI_EARLY", "1") != "0"
+        if rccl_early:
+            # bucket 0 (fc, 4.7 MB) is complete: its all-reduce goes out now, on the
+            # high-priority comm stream, beside the conv backward
+            self.reducer.bucket_ready(0)
         if early:
             # bucket 0 (fc, 4.7 MB) is complete: its xGMI all-reduce kernel is small enough
             # to be co-resident with cnn_bwd, so it travels during the conv backward
@@ -360,6 +373,13 @@ class CnnStep(GpuStepBase):
         # for cnn_bwd or push part of it into a second round.  The small conv bucket goes
         # first (the next forward needs it); the 4.7 MB fc bucket keeps reducing while the
         # conv update and the next step's cnn_fwd run.
+        if rccl_early:
+            # the fc bucket is already on the wire; the conv bucket queues behind it on the
+            # comm stream; one optimizer launch once both have landed
+            self.reducer.bucket_ready(1)
+            self.reducer.finalize()
+            self.launch_optimizer()
+            return
         if not self.fc_carry:
             # one grouped RCCL launch for both buckets, one optimizer launch for everything
             self.reducer.all_ready()
@@ -411,8 +431,22 @@ class CnnStep(GpuStepBase):
         super().invalidate_graphs()
         self._bsegs = None
         self._fused = {}
-        self.phase_period = 2 if self._wt_double_on() else 1
-        self.phase %= self.phase_period
+        period = 2 if self._wt_double_on() else 1
+        if self.phase != self.phase % period:
+            # leaving double-buffer mode at phase 1: the newest W1^T is in copy 1, and every
+            # single-buffer path reads copy 0
+            self.wf1t2[0].copy_(self.wf1t2[self.phase])
+        self.phase_period = period
+        self.phase %= period
+        self._poison_unkept_grads()
+
+    def _poison_unkept_grads(self) -> None:
+        """With the fused fc1 update and keep_grads off, fc1_bwd consumes the fc1-weight
+        gradient in registers and never stores it: fill that slice of the gradient arena with
+        NaN so a later reader (norm logging, clipping, dumps) fails visibly instead of seeing
+        a stale step's values."""
+        if self.fuse_fc1 and self.fuse_conv_reduce and not self.keep_grads:
+            self.G["fc1.weight"].fill_(float("nan"))
 
     def evaluate(self) -> None:
         C, P = self.C, self.P

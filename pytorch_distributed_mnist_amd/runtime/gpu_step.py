@@ -25,6 +25,10 @@ from ..ops import _ext
 
 
 _GRAPH_STEPS = int(os.environ.get("PDM_GRAPH_STEPS", "8"))   # steps per graph: a power of two
+if _GRAPH_STEPS <= 0 or _GRAPH_STEPS & (_GRAPH_STEPS - 1):
+    # train_steps splits a remainder into the set bits of GRAPH_SIZES: other sizes would
+    # replay the wrong number of steps and desynchronise the device and host counters
+    raise ValueError(f"PDM_GRAPH_STEPS must be a power of two, got {_GRAPH_STEPS}")
 
 
 def make_gpu_step(prog, use_graphs: bool = True):
@@ -97,6 +101,9 @@ class GpuStepBase:
         next's)."""
         n = idx.numel()
         if self._ring is None or self._ring[0][0].numel() != n:
+            for old in self._ring or ():
+                if old[1] is not None:   # a queued gather still reads this pinned buffer
+                    old[1].synchronize()
             self._ring = [[torch.empty(n, dtype=torch.int32, pin_memory=True), None]
                           for _ in range(3)]
             self._ring_i = 0
@@ -142,6 +149,11 @@ class GpuStepBase:
         n = idx_cpu.numel()
         cur = torch.cuda.current_stream(self.device)
         if self._n_epoch != n:
+            p = self._pending
+            if p is not None and p[2] is not None:
+                # an ahead gather still writes the old epoch buffer and reads a pinned buffer
+                # of the ring about to be replaced: drain it before either is freed
+                p[2].synchronize()
             self.ep_images = torch.empty(2 * n * 784, dtype=torch.uint8, device=self.device)
             self.ep_labels = torch.empty(2 * n, dtype=torch.int32, device=self.device)
             self._n_epoch = n
@@ -230,13 +242,15 @@ class GpuStepBase:
         self._graph(B, nsteps).replay()
         self.phase = (self.phase + nsteps) % self.phase_period
 
-    def prepare(self, B: int) -> None:
-        """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, both
-        step phases), so no capture or first-launch upload lands inside a timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
+    def prepare(self, B: int, sizes=None) -> None:
+        """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, or
+        `sizes`, in every step phase), so no capture or first-launch upload lands inside a
+        timed run.  Capturing enqueues nothing; the graphs' steps read the device counters
         when replayed."""
         if not self.use_graphs:
             return
-        for n, ph in ((n, ph) for n in self.GRAPH_SIZES for ph in range(self.phase_period)):
+        for n, ph in ((n, ph) for n in (sizes or self.GRAPH_SIZES)
+                      for ph in range(self.phase_period)):
             g = self._graph(B, n, ph)
             try:
                 exe = g.raw_cuda_graph_exec()

@@ -24,8 +24,14 @@ def test_bench_json_contract(gpu):
     assert d["scaling"] == "weak" and d["dtype"] == "bf16" and d["data"].startswith("synthetic")
     assert d["config"]["model"] == "mnist_cnn" and d["config"]["parallelism"] == "dp1"
     assert d["value"] > 0 and d["ms_per_step"] > 0
-    # value is the whole-job images/sec implied by the timed steps
-    assert abs(d["value"] - d["config"]["global_batch"] / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
+    # value is the whole-job images/sec of the timed steps: the reference's epoch sequence
+    # (full batches, then the 96-image ragged tail of 60000 / 256) with a boundary inside
+    c = d["config"]
+    assert c["epoch_steps"] == 235 and c["tail_batch_per_rank"] == 96
+    assert c["images_timed"] == 19 * 256 + 96
+    el = d["ms_per_step"] * d["steps"] / 1e3
+    assert abs(d["value"] - c["images_timed"] / el) / d["value"] < 0.01
+    assert d["launch"] == "single" and isinstance(d["knobs"], dict)
     assert d["vs_baseline"] > 1.0
     # an epoch boundary (next epoch's sampler order: upload + gather) falls in the window
     assert d["config"]["epoch_boundaries_timed"] >= 1
@@ -45,7 +51,7 @@ def test_bench_transport_calibration(gpu):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     cal = d["config"]["transport_calibration_ms_per_step"]
-    assert set(cal) == {"xgmi", "rccl", "rccl-nocarry", "rccl-side"}, cal
+    assert set(cal) == {"xgmi", "rccl", "rccl-nocarry", "rccl-side", "rccl-early"}, cal
     assert d["config"]["grad_transport"] == min(cal, key=cal.get)
     # what the data plane saw: a 1-rank RCCL communicator, no xGMI peer to map
     assert d["comm"]["rccl_comm_count"] == 1
@@ -88,3 +94,21 @@ def test_bench_two_rank_xgmi_rehearsal(gpu):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["grad_transport"] == "xgmi"
+
+
+def test_bench_self_spawn_rehearsal(gpu):
+    """`python bench.py --gpus 2` with no launcher starts its two ranks itself (before any GPU
+    call) and forwards rank 0's one JSON line; rehearsed on one GPU over gloo."""
+    env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_BENCH_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--steps", "20", "--warmup", "5"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["launch"] == "spawned"
+    assert d["config"]["parallelism"] == "dp2" and d["strong"]["batch_per_rank"] == 128
+    assert d["knobs"] == {"PDM_BENCH_BACKEND": "gloo", "PDM_SHARE_DEVICE": "1"}

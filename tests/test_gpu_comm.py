@@ -74,7 +74,7 @@ def test_grad_reducer_grouped_all_ready(gpu):
     comm.close()
 
 
-@pytest.mark.parametrize("carry", ["carry", "nocarry", "side"])
+@pytest.mark.parametrize("carry", ["carry", "nocarry", "side", "early"])
 @pytest.mark.parametrize("B", [256, 32])
 def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
     """The world_size > 1 step structure (unfused conv reduction, grouped RCCL all-reduce of
@@ -92,8 +92,9 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
                                 momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=force,
                                 transport="rccl")
         assert p.gpu.fuse_conv_reduce == (not force)
-        p.gpu.fc_carry = carry != "nocarry"
+        p.gpu.fc_carry = carry not in ("nocarry", "early")
         p.gpu.fc_side = carry == "side"
+        p.gpu.fc_early = carry == "early"
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         p.train_epoch()

@@ -1,0 +1,20 @@
+# Round 4 probe: warm-up ramp of the driver's 20-step window, PMC tables (B=256 bf16,
+# B=32 bf16 through the N>1 chain, fp32 B=256) and an in-step trace of the fp32 bench.
+set -o pipefail
+O=gpurun_out/r4a
+mkdir -p $O
+export TMPDIR=/tmp
+: > $O/warm.jsonl
+for W in 5 50 500 5; do
+  timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup $W >> $O/warm.jsonl 2>> $O/bench.err || exit 1
+done
+timeout -k 10 240 python bench.py --dtype fp32 >> $O/warm.jsonl 2>> $O/bench.err || exit 1
+bash tools/pmc_run.sh b256 256 bf16 > $O/pmc_b256.log 2>&1 || exit 1
+bash tools/pmc_run.sh b32force 32 bf16 force > $O/pmc_b32.log 2>&1 || exit 1
+bash tools/pmc_run.sh f32 256 fp32 > $O/pmc_f32.log 2>&1 || exit 1
+cp gpurun_out/pmc/*.md $O/
+d=$O/trace_f32
+timeout -k 10 180 rocprofv3 --kernel-trace -d $d -o run -- python3 bench.py --dtype fp32 --steps 200 --warmup 30 > /dev/null 2>&1 || exit 1
+python tools/rocpd_summary.py $(ls $d/*.db) --title "in-step kernels, bench.py --dtype fp32 B=256, 200 steps" --steps 150 > $O/trace_f32.md && rm -rf $d
+rm -rf gpurun_out/pmc
+echo done

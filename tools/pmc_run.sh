@@ -1,19 +1,26 @@
 #!/bin/bash
-# PMC counter passes over tools/step_loop.py (eager CNN steps, B=256), one rocprofv3 run per
-# pass (counter slots per pass: MI355X_MICROARCH.md "rocprofv3 PMC slots"), then a table.
-# Run on the GPU box:  bash tools/pmc_run.sh  -> gpurun_out/pmc/*, gpurun_out/pmc.md
+# PMC counter passes over tools/step_loop.py (eager steps), one rocprofv3 run per pass
+# (counter slots per pass: MI355X_MICROARCH.md "rocprofv3 PMC slots"), plus a kernel-trace
+# run for durations, then the derived per-kernel table (tools/pmc_table.py).
+#   bash tools/pmc_run.sh NAME B DTYPE [force]   -> gpurun_out/pmc/NAME/*, gpurun_out/pmc/NAME.md
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-out=gpurun_out/pmc
+name=${1:-b256}; B=${2:-256}; DT=${3:-bf16}; FORCE=${4:-}
+out=gpurun_out/pmc/$name
 mkdir -p "$out"
+prog="python3 tools/step_loop.py $B 30 $DT $FORCE"
 pass() {
-  local name=$1; shift
-  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run \
-    -- python3 tools/step_loop.py 256 30 > "$out/$name.log" 2>&1
+  local p=$1; shift
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$out/$p" -o run \
+    -- $prog > "$out/$p.log" 2>&1
 }
 pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT \
   SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE
-pass rd FETCH_SIZE GRBM_COUNT
-pass wr WRITE_SIZE TCC_HIT_sum
-python3 tools/pmc_summary.py $(find "$out" -name '*counter_collection.csv') > gpurun_out/pmc.md
+pass st SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES
+pass rd FETCH_SIZE
+pass wr WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
+timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d "$out/trace" -o run \
+  -- $prog > "$out/trace.log" 2>&1
+python3 tools/pmc_table.py --title "$name: eager steps, B=$B, $DT $FORCE (30 steps, means per dispatch)" \
+  --trace "$out/trace" "$out/sq" "$out/st" "$out/rd" "$out/wr" > gpurun_out/pmc/$name.md

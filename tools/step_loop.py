@@ -1,5 +1,10 @@
 """Run N eager (no hipGraph) CNN training steps at batch B: a plain target for rocprofv3
-counter collection (python3 tools/step_loop.py [B] [N])."""
+counter collection.
+
+    python3 tools/step_loop.py [B] [N] [bf16|fp32] [force]
+
+`force` runs the world-size>1 step structure through a 1-rank RCCL communicator
+(unfused conv reduction, bucket all-reduces), as bench.py's PDM_FORCE_COMM=1."""
 import os
 import sys
 
@@ -12,13 +17,20 @@ from pytorch_distributed_mnist_amd.runtime.program import build_local_program  #
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+DT = sys.argv[3] if len(sys.argv) > 3 else "bf16"
+FORCE = len(sys.argv) > 4 and sys.argv[4] == "force"
 train = synthetic_split(60000, True)
 test = synthetic_split(512, False)
-p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.01,
-                        use_graphs=False)
+comm = None
+if FORCE:
+    from pytorch_distributed_mnist_amd.parallel.comm import RcclComm
+    comm = RcclComm(0, 1, torch.device("cuda", 0))
+p = build_local_program("cnn", DT, "cuda", B, train, test, optimizer="sgd", lr=0.01,
+                        use_graphs=False, comm=comm, force_comm=FORCE,
+                        transport="rccl" if FORCE else None)
 p.optimizer.sync_hyperparams()
 p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
 for _ in range(N):
     p.gpu.train_step(B)
 torch.cuda.synchronize()
-print("done", B, N)
+print("done", B, N, DT, "force" if FORCE else "")
