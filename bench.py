@@ -311,7 +311,11 @@ def main():
             torch.cuda.synchronize()
             return allmax(time.perf_counter() - t0), imgs
 
+        shardable = hasattr(prog.gpu, "set_shard_fc")
+
         def use(red, carry="carry"):
+            if shardable:
+                prog.gpu.set_shard_fc(False)   # (gathers the sharded state on the old reducer)
             prog.reducer = red
             prog.gpu.reducer = red
             prog.gpu.use_graphs = bool(a.graphs) and red.capturable
@@ -320,6 +324,9 @@ def main():
                 prog.gpu.fc_side = carry == "side"
                 prog.gpu.fc_early = carry == "early"
             prog.gpu.invalidate_graphs()
+            if shardable and (carry == "zero" or os.environ.get("PDM_SHARD_FC") == "1") and \
+                    red.active and prog.gpu.shard_supported():
+                prog.gpu.set_shard_fc(True)
 
         def prepare():
             """Capture + upload the step graphs outside any timed window (a graph captured
@@ -336,6 +343,10 @@ def main():
             if name == "rccl" and model == "cnn" and os.environ.get("PDM_FC_CARRY") is None:
                 cands += [("rccl", red, "carry"), ("rccl-nocarry", red, "nocarry"),
                           ("rccl-side", red, "side"), ("rccl-early", red, "early")]
+                if shardable and prog.gpu.shard_supported(red):
+                    # fc1 optimizer-state sharding: reduce-scatter + sharded update + bf16
+                    # all-gather (CnnStep.set_shard_fc)
+                    cands.append(("rccl-zero", red, "zero"))
             else:
                 env = os.environ.get("PDM_FC_CARRY", "1") != "0"
                 side = os.environ.get("PDM_FC_SIDE", "0") == "1"
@@ -367,6 +378,8 @@ def main():
                         raise RuntimeError("rccl transport failed calibration")
                     del calib[name]
                     sync("recovery")
+                    if shardable:
+                        prog.gpu.set_shard_fc(False)
                     # replicas (and their momentum) may differ after a failed reduce
                     for t in (arena.params, *opt.state_buffers().values()):
                         comm.broadcast_(t, 0)
@@ -398,10 +411,14 @@ def main():
         boundaries = -(-(a.steps - left) // spe) if a.steps > left else 0
         elapsed, imgs = timed(a.steps)
         chosen.check()
+        prog.sync_master()
         if not torch.isfinite(arena.params).all():
             raise RuntimeError("non-finite parameters after the benchmark")
         ms = elapsed / a.steps * 1e3
-        return {"B": B, "global_batch": B * ws, "elapsed": elapsed, "ms": ms,
+        sharded = bool(getattr(prog.gpu, "shard_fc", False))
+        if shardable:
+            prog.gpu.set_shard_fc(False)
+        return {"B": B, "global_batch": B * ws, "elapsed": elapsed, "ms": ms, "shard_fc": sharded,
                 "value": imgs * ws / elapsed, "images": imgs * ws, "tail": tail,
                 "epoch_steps": spe, "transport": best,
                 "calib": {k: round(v, 5) for k, v in calib.items()},
@@ -446,6 +463,7 @@ def main():
                        "transport_calibration_ms_per_step": m["calib"],
                        "epoch_boundaries_timed": m["epoch_boundaries_timed"],
                        "epoch_steps": m["epoch_steps"], "tail_batch_per_rank": m["tail"],
+                       "fc1_update_sharded": m["shard_fc"],
                        "images_timed": m["images"]},
             "value_semantics": (
                 "weak scaling: images/sec of the whole node at a fixed per-rank batch; timed "

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   }
 
   const Hyper h = make_hyper<KIND>(a);
-  if (s.shadow_t == nullptr) {
+  if (s.shadow_t == nullptr && !s.sfrag) {
     // plain segment: 8 contiguous floats per thread (2 x float4)
     const int64_t e0 = (int64_t)lb * CHUNK + threadIdx.x * 8;
 #pragma unroll
@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       }
     }
   }
+  if (s.shadow_t == nullptr) return;   // fragment-major shadow only (a row shard of W1)
   __syncthreads();
   // transposed store: thread -> (col c, 8 consecutive rows) = one 16-B store
   const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 8;
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
 
 int opt_blocks_for(const OptSeg& s) {
   if (s.slab) return (int)(((int64_t)s.rows * s.cols + 63) / 64);
-  if (s.shadow_t || s.tonly) return ((s.rows + TR - 1) / TR) * ((s.cols + TC - 1) / TC);
+  if (s.shadow_t || s.tonly || s.sfrag) return ((s.rows + TR - 1) / TR) * ((s.cols + TC - 1) / TC);
   const int64_t n = (int64_t)s.rows * s.cols;
   return (int)((n + CHUNK - 1) / CHUNK);
 }

@@ -215,6 +215,22 @@ class RcclComm {
     enqueued(ncclAllReduce(ptr, ptr, count, dt, ncclSum, comm_, stream_), "bucket all-reduce");
   }
 
+  // in place over [ptr, ptr + nranks * count): rank r's sum lands in its own slice
+  // [ptr + r * count, ...); the other slices keep unspecified partial values
+  void reduce_scatter_range(float* ptr, size_t count) {
+    alive();
+    enqueued(ncclReduceScatter(ptr, ptr + (size_t)rank_ * count, count, ncclFloat32, ncclSum, comm_,
+                               stream_), "bucket reduce-scatter");
+  }
+
+  // in place over [ptr, ptr + nranks * count * elem): every rank's slice to every rank
+  void all_gather_range(void* ptr, size_t count, ncclDataType_t dt, size_t elem) {
+    alive();
+    char* base = static_cast<char*>(ptr);
+    enqueued(ncclAllGather(base + (size_t)rank_ * count * elem, base, count, dt, comm_, stream_),
+             "shard all-gather");
+  }
+
   void broadcast_(at::Tensor t, int root) {
     check_dev(t, device_);
     alive();
@@ -280,20 +296,44 @@ class GradReducer {
     reduced_.resize(starts_.size());
     for (auto& e : reduced_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&gready_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&gdone_, hipEventDisableTiming));
   }
   ~GradReducer() {
     for (auto& e : ready_) hipEventDestroy(e);
     for (auto& e : reduced_) hipEventDestroy(e);
     hipEventDestroy(done_);
+    hipEventDestroy(gready_);
+    hipEventDestroy(gdone_);
   }
+
+  // Shard part of bucket i (ZeRO-1 style, optimizer-state sharding on one bucket): the
+  // `nranks * count` floats at `start` are reduce-scattered (rank r receives the sum of
+  // slice r only, which is all its optimizer update reads), the rest of the bucket is
+  // all-reduced as before; both in one RCCL group.
+  void set_shard(int i, int64_t start, int64_t count) {
+    TORCH_CHECK(i >= 0 && i < (int)starts_.size(), "bad bucket index");
+    const int64_t n = (int64_t)comm_.size() * count;
+    TORCH_CHECK(count > 0 && start >= starts_[i] && start + n <= starts_[i] + counts_[i],
+                "shard outside its bucket");
+    shard_bucket_ = i;
+    shard_start_ = start;
+    shard_count_ = count;
+  }
+  void clear_shard() { shard_bucket_ = -1; }
 
   void bucket_ready(int i) {
     TORCH_CHECK(i >= 0 && i < (int)starts_.size(), "bad bucket index");
     hipStream_t cur = comm_.caller();
     HIP_OK(hipEventRecord(ready_[i], cur));
     HIP_OK(hipStreamWaitEvent(comm_.stream(), ready_[i], 0));
-    float* base = grads_.data_ptr<float>() + starts_[i];
-    comm_.all_reduce_range(base, (size_t)counts_[i], ncclFloat32);
+    if (i == shard_bucket_) {
+      NCCL_OK(ncclGroupStart());
+      enqueue_bucket(i);
+      comm_.enqueued(ncclGroupEnd(), "grouped sharded bucket");
+    } else {
+      enqueue_bucket(i);
+    }
     HIP_OK(hipEventRecord(reduced_[i], comm_.stream()));
     pending_ = true;
   }
@@ -305,12 +345,25 @@ class GradReducer {
     HIP_OK(hipEventRecord(ready_[0], cur));
     HIP_OK(hipStreamWaitEvent(comm_.stream(), ready_[0], 0));
     NCCL_OK(ncclGroupStart());
-    for (size_t i = 0; i < starts_.size(); ++i)
-      comm_.all_reduce_range(grads_.data_ptr<float>() + starts_[i], (size_t)counts_[i], ncclFloat32);
+    for (size_t i = 0; i < starts_.size(); ++i) enqueue_bucket((int)i);
     comm_.enqueued(ncclGroupEnd(), "grouped bucket all-reduce");
     for (auto& e : reduced_) HIP_OK(hipEventRecord(e, comm_.stream()));
     pending_ = true;
   }
+
+  // in-place all-gather of `t` (rank r owns t's slice r of nranks equal slices) on the comm
+  // stream, after the caller's current stream; wait_gather() joins it back
+  void gather(at::Tensor t) {
+    check_dev(t, comm_.device());
+    const int64_t n = comm_.size();
+    TORCH_CHECK(t.numel() % n == 0, "all-gather tensor must split into ", n, " equal slices");
+    hipStream_t cur = comm_.caller();
+    HIP_OK(hipEventRecord(gready_, cur));
+    HIP_OK(hipStreamWaitEvent(comm_.stream(), gready_, 0));
+    comm_.all_gather_range(t.data_ptr(), (size_t)(t.numel() / n), nccl_dtype(t), t.element_size());
+    HIP_OK(hipEventRecord(gdone_, comm_.stream()));
+  }
+  void wait_gather() { HIP_OK(hipStreamWaitEvent(comm_.caller(), gdone_, 0)); }
 
   // make the caller's current stream wait for bucket i's all-reduce only (e.g. a side
   // stream running that bucket's optimizer while later backward kernels still run)
@@ -330,12 +383,28 @@ class GradReducer {
   int num_buckets() const { return (int)starts_.size(); }
 
  private:
+  // the collectives of bucket i (inside the caller's group when sharded)
+  void enqueue_bucket(int i) {
+    float* g = grads_.data_ptr<float>();
+    const int64_t s = starts_[i], e = starts_[i] + counts_[i];
+    if (i != shard_bucket_) {
+      comm_.all_reduce_range(g + s, (size_t)counts_[i], ncclFloat32);
+      return;
+    }
+    const int64_t ss = shard_start_, se = shard_start_ + (int64_t)comm_.size() * shard_count_;
+    if (ss > s) comm_.all_reduce_range(g + s, (size_t)(ss - s), ncclFloat32);
+    comm_.reduce_scatter_range(g + ss, (size_t)shard_count_);
+    if (e > se) comm_.all_reduce_range(g + se, (size_t)(e - se), ncclFloat32);
+  }
+
   RcclComm& comm_;
   at::Tensor grads_;
   std::vector<int64_t> starts_, counts_;
   std::vector<hipEvent_t> ready_, reduced_;
-  hipEvent_t done_ = nullptr;
+  hipEvent_t done_ = nullptr, gready_ = nullptr, gdone_ = nullptr;
   bool pending_ = false;
+  int shard_bucket_ = -1;
+  int64_t shard_start_ = 0, shard_count_ = 0;
 };
 
 void register_comm(py::module& m) {
@@ -368,5 +437,9 @@ void register_comm(py::module& m) {
       .def("finalize", &GradReducer::finalize)
       .def("wait_bucket", &GradReducer::wait_bucket)
       .def("all_ready", &GradReducer::all_ready)
+      .def("set_shard", &GradReducer::set_shard)
+      .def("clear_shard", &GradReducer::clear_shard)
+      .def("gather", &GradReducer::gather)
+      .def("wait_gather", &GradReducer::wait_gather)
       .def_property_readonly("num_buckets", &GradReducer::num_buckets);
 }

@@ -149,6 +149,12 @@ def run(args):
         # every host sync of the epoch loop waits at most --timeout for the device (and the
         # collectives it is queued behind), then aborts the communicator and raises
         program.sync_fn = lambda what: parallel.bounded_sync(device, args.timeout, comm, what)
+    if getattr(args, "shard_fc", False) and world_size > 1:
+        if program.shard_supported():
+            program.set_shard_fc(True)
+        elif rank == 0:
+            out("warning: --shard-fc needs the CNN over rccl or gloo with a world size that "
+                "splits fc1's 128 rows evenly (16-row shards on the GPU); running unsharded")
     trainer = Trainer(program)
 
     try:
@@ -181,6 +187,7 @@ def run(args):
 
                 is_best = test_acc.accuracy > best_acc
                 best_acc = max(test_acc.accuracy, best_acc)
+                program.sync_master()       # sharded state: every rank gathers the full state
                 if rank == 0:
                     with trace.range("checkpoint"):
                         save_checkpoint(make_state(epoch + 1, arena, best_acc, optimizer), is_best,

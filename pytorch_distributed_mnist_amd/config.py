@@ -76,6 +76,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help='gradient all-reduce transport on GPU with --backend nccl: xgmi = direct '
                         'peer-to-peer pushes over xGMI (hipIpc), rccl = ncclAllReduce; auto '
                         '(default, or $PDM_COMM) = xgmi when every rank passes its self-check')
+    g.add_argument('--shard-fc', action='store_true',
+                   help='bf16 CNN, world size > 1 over rccl (or gloo): shard the fc1 weight\'s '
+                        'optimizer update over the ranks (reduce-scatter of its gradient, each '
+                        'rank updates 128 / world_size rows, all-gather of the bf16 rows); '
+                        'checkpoints gather the full state first and keep the reference format')
     g.add_argument('--checkpoint-dir', default='checkpoints')
     g.add_argument('--timeout', type=float, default=1800.0,
                    help='deadline in seconds for the rendezvous, RCCL communicator init and every '

@@ -83,6 +83,19 @@ class FlatOptimizer:
     def state_buffers(self) -> Dict[str, torch.Tensor]:
         raise NotImplementedError
 
+    def _freeze(self, frozen):
+        """Save the [start, end) ranges of the parameters and optimizer state that this step
+        must leave unchanged (another rank's shard); returns a restore function."""
+        if not frozen:
+            return lambda: None
+        bufs = [self.arena.params, *self.state_buffers().values()]
+        saved = [(b, s, e, b[s:e].clone()) for b in bufs for s, e in frozen if e > s]
+
+        def restore():
+            for b, s, e, v in saved:
+                b[s:e].copy_(v)
+        return restore
+
     def zero_grad(self, set_to_none: bool = True) -> None:
         # Gradients are overwritten (not accumulated) by the backward kernels,
         # so there is nothing to clear; kept for API parity with torch.optim.
@@ -107,8 +120,13 @@ class FlatAdam(FlatOptimizer):
     def state_buffers(self):
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
 
-    def step_cpu(self, grad_scale: float = 1.0) -> None:
+    def step_cpu(self, grad_scale: float = 1.0, frozen=None) -> None:
         """torch ``_single_tensor_adam`` math on the flat buffers (CPU path)."""
+        restore = self._freeze(frozen)
+        self._adam_cpu(grad_scale)
+        restore()
+
+    def _adam_cpu(self, grad_scale):
         g0 = self.param_groups[0]
         beta1, beta2 = g0["betas"]
         lr, eps, wd = g0["lr"], g0["eps"], g0["weight_decay"]
@@ -179,8 +197,13 @@ class FlatSGD(FlatOptimizer):
     def state_buffers(self):
         return {"momentum_buffer": self.momentum_buffer}
 
-    def step_cpu(self, grad_scale: float = 1.0) -> None:
+    def step_cpu(self, grad_scale: float = 1.0, frozen=None) -> None:
         """torch ``_single_tensor_sgd`` math on the flat buffers (CPU path)."""
+        restore = self._freeze(frozen)
+        self._sgd_cpu(grad_scale)
+        restore()
+
+    def _sgd_cpu(self, grad_scale):
         g0 = self.param_groups[0]
         lr, mom, wd = g0["lr"], g0["momentum"], g0["weight_decay"]
         damp, nesterov = g0["dampening"], g0["nesterov"]

@@ -170,6 +170,50 @@ class GradReducer:
             w.wait()
         self._pending.clear()
 
+    # -- optimizer-state sharding of one bucket (ZeRO-1 on the fc bucket) ------------------
+    shard = None              # (bucket, start, count per rank) when set
+
+    @property
+    def can_shard(self) -> bool:
+        """Reduce-scatter + all-gather exist on this data plane (RCCL, or the gloo/torch
+        rehearsal path); the direct xGMI all-reduce has no sharded form."""
+        return self.active and (self.kind == "rccl" or self.kind == "torch")
+
+    def set_shard(self, bucket: int, start: int, count: int) -> None:
+        """Reduce-scatter the ``world_size * count`` floats of bucket `bucket` at `start`
+        (rank r then holds the summed slice r) and all-reduce the rest of the bucket."""
+        if not self.can_shard:
+            raise RuntimeError(f"the {self.kind} transport cannot shard a bucket")
+        s, e = self.bounds[bucket]
+        if not (s <= start and start + self.comm.world_size * count <= e and count > 0):
+            raise ValueError("shard outside its bucket")
+        self.shard = (bucket, start, count)
+        if self._native is not None:
+            self._native.set_shard(bucket, start, count)
+
+    def clear_shard(self) -> None:
+        self.shard = None
+        if self._native is not None:
+            self._native.clear_shard()
+
+    def gather(self, t: torch.Tensor) -> None:
+        """In-place all-gather: rank r owns slice r of ``world_size`` equal slices of `t`
+        (e.g. its rows of the bf16 W1 copy after a sharded update).  Native: on the comm
+        stream behind the caller's stream; ``wait_gather`` joins it back."""
+        if not self.active:
+            return
+        if self._native is not None:
+            self._native.gather(t)
+            return
+        ws = self.comm.world_size
+        parts = list(t.view(ws, -1).unbind(0))
+        mine = parts[self.comm.rank].clone()
+        torch.distributed.all_gather(parts, mine)      # gloo: copies into t's slices
+
+    def wait_gather(self) -> None:
+        if self.active and self._native is not None:
+            self._native.wait_gather()
+
     def check(self) -> None:
         """Raise if the xgmi transport reported a peer timeout (no-op otherwise)."""
         if self.kind == "xgmi":

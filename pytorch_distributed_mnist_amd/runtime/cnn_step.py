@@ -193,14 +193,80 @@ class CnnStep(GpuStepBase):
         # free for RCCL's kernel (B = 32: 192 workgroups on 256 CUs); at B = 256 cnn_bwd takes
         # every CU and the collective waits for it.  bench.py calibrates it as well.
         self.fc_early = os.environ.get("PDM_FC_EARLY", "0") == "1"
+        # world_size > 1: optimizer-state sharding of the fc1 weight (set_shard_fc): its
+        # gradient is reduce-scattered instead of all-reduced, each rank updates its
+        # 128 / world_size rows (fp32 master, momentum, bf16 W1 rows) and the bf16 W1 rows are
+        # all-gathered; W1^T is re-derived locally.  Same arithmetic per element as the
+        # replicated update; the fp32 rows a rank does not own go stale until sync_master()
+        # (checkpoints, evaluation of the fp32 weights, parameter checks)
+        self.shard_fc = False
+        self._shard_rows = None
         self._side = None
         self._side_ev = None
         self.refresh_shadows()
         self._poison_unkept_grads()
 
+    # -- fc1 optimizer-state sharding --------------------------------------------------------
+    def shard_supported(self, reducer=None) -> bool:
+        red = reducer or self.reducer
+        ws = red.comm.world_size
+        return red.can_shard and 128 % ws == 0 and (128 // ws) % 16 == 0
+
+    def set_shard_fc(self, on: bool) -> None:
+        """Switch the fc1-weight optimizer-state sharding on or off (graphs are re-captured)."""
+        if bool(on) == self.shard_fc:
+            return
+        if on:
+            if not self.shard_supported():
+                raise RuntimeError("fc1 sharding needs an RCCL or gloo data plane and a world "
+                                   "size that splits 128 rows into multiples of 16")
+            ws, r = self.reducer.comm.world_size, self.reducer.comm.rank
+            rows = 128 // ws
+            self.reducer.set_shard(0, self.arena.spec.offset("fc1.weight"), rows * 9216)
+            self._shard_rows = (r * rows, rows)
+            self.shard_fc = True
+        else:
+            self.sync_master()
+            self.reducer.clear_shard()
+            self.shard_fc = False
+            self._shard_rows = None
+        self.invalidate_graphs()
+
+    @torch.no_grad()
+    def sync_master(self) -> None:
+        """Sharded mode: all-gather the fp32 fc1 rows and their optimizer state, so every
+        rank holds the full, current master weights (collective: every rank calls it)."""
+        if not self.shard_fc:
+            return
+        off, n = self.arena.spec.offset("fc1.weight"), 128 * 9216
+        for buf in (self.arena.params, *self.opt.state_buffers().values()):
+            self.reducer.gather(buf[off:off + n])
+        self.reducer.wait_gather()
+
+    def _shard_segments(self):
+        """Optimizer segments of a sharded step: every parameter but fc1.weight whole, and this
+        rank's rows of fc1.weight (fp32 update + its rows of the fragment-major bf16 W1, which
+        start on a 16-row fragment boundary); plus the transpose-only W1 -> W1^T segment run
+        after the all-gather."""
+        if getattr(self, "_ssegs", None) is None:
+            off1 = self.arena.spec.offset("fc1.weight")
+            r0, rows = self._shard_rows
+            segs = []
+            for sg in self.optimizer_segments():
+                if sg[0] == off1:
+                    segs.append((off1 + r0 * 9216, rows, 9216,
+                                 self.wf1[r0 * 9216:(r0 + rows) * 9216], None, None, False, False,
+                                 True))
+                else:
+                    segs.append(sg)
+            tseg = [(off1, 128, 9216, self.wf1, self.wf1t, None, True, True, True)]
+            self._ssegs = (segs, tseg)
+        return self._ssegs
+
     @torch.no_grad()
     def refresh_shadows(self) -> None:
         """Re-derive the bf16 weight copies from the fp32 master weights."""
+        self.sync_master()
         w1 = self.arena.param("fc1.weight").reshape(128, 9216)
         self.wf1.copy_(frag_major(w1.to(torch.bfloat16)))
         wt = frag_major_t(w1.to(torch.bfloat16))
@@ -281,8 +347,9 @@ class CnnStep(GpuStepBase):
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
-        carry = (self.reducer.active and getattr(self.reducer, "kind", None) == "rccl" and
-                 self.fc_carry and not self.fc_early)
+        rccl = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
+        # sharded: the W1 all-gather and the W1^T transpose are carried past the next cnn_fwd
+        carry = rccl and (self.shard_fc or (self.fc_carry and not self.fc_early))
         streamed = self.reducer.streamed
         if streamed:
             self.reducer.begin(n)        # one persistent xgmi collective for the n steps
@@ -308,7 +375,10 @@ class CnnStep(GpuStepBase):
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
                   self.pmask, *self.fwd_outputs(B), spe=self.spe)
-        if carry_in and self.fc_side:
+        if carry_in and self.shard_fc:
+            self.reducer.wait_gather()                # this step's W1 rows from every rank
+            self.launch_optimizer(self._shard_segments()[1])
+        elif carry_in and self.fc_side:
             torch.cuda.current_stream(self.device).wait_event(self._side_ev)
         elif carry_in:
             self.reducer.wait_bucket(0)
@@ -345,6 +415,21 @@ class CnnStep(GpuStepBase):
             return
         C.conv_reduce(self.conv_slab, nblk, G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
+        if self.shard_fc:
+            # fc bucket: reduce-scatter of the fc1 weight + all-reduce of fc2 / fc1 bias (one
+            # RCCL group, already on the wire if rccl_early), conv bucket all-reduced; one
+            # update of every parameter but the other ranks' fc1 rows; W1 rows all-gathered
+            if not rccl_early:
+                self.reducer.bucket_ready(0)
+            self.reducer.bucket_ready(1)
+            self.reducer.finalize()
+            segs, tseg = self._shard_segments()
+            self.launch_optimizer(segs)
+            self.reducer.gather(self.wf1)
+            if not carry_out:
+                self.reducer.wait_gather()
+                self.launch_optimizer(tseg)
+            return
         if xgmi and red.streamed:
             # the optimizer publishes the conv bucket; its fc workgroups wait for bucket 0
             # (long reduced by now), its conv workgroups for bucket 1
@@ -430,6 +515,7 @@ class CnnStep(GpuStepBase):
     def invalidate_graphs(self) -> None:
         super().invalidate_graphs()
         self._bsegs = None
+        self._ssegs = None
         self._fused = {}
         period = 2 if self._wt_double_on() else 1
         if self.phase != self.phase % period:

@@ -40,7 +40,18 @@ def train_step_cpu(model: str, arena, images_u8, labels, reducer, optimizer, met
         for b in range(reducer.num_buckets):
             reducer.bucket_ready(b)
         reducer.finalize()
-        optimizer.step_cpu(grad_scale=reducer.grad_scale)
+        sh = getattr(reducer, "shard", None)
+        if sh is None:
+            optimizer.step_cpu(grad_scale=reducer.grad_scale)
+        else:
+            # sharded fc1 update: this rank's rows only (the other rows and their optimizer
+            # state are left as they are), then every rank's updated rows all-gathered
+            _, start, count = sh
+            ws, r = reducer.comm.world_size, reducer.comm.rank
+            own = (start + r * count, start + (r + 1) * count)
+            frozen = [(start, own[0]), (own[1], start + ws * count)]
+            optimizer.step_cpu(grad_scale=reducer.grad_scale, frozen=frozen)
+            reducer.gather(arena.params[start:start + ws * count])
         bsz = images_u8.shape[0]
         correct = logits.argmax(dim=1).eq(labels).sum().item()
         metrics_buf[0] += loss.item() * bsz

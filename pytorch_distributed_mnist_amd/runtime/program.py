@@ -94,6 +94,45 @@ class TrainProgram:
                                self.train_split.labels[idx], self.reducer, self.optimizer, buf)
         return self.metrics.read(DeviceMetrics.TRAIN)
 
+    # -- fc1 optimizer-state sharding (CNN, world size > 1) ------------------------------------
+    def shard_supported(self) -> bool:
+        if self.model != "cnn":
+            return False
+        if self.gpu is not None:
+            return hasattr(self.gpu, "shard_supported") and self.gpu.shard_supported()
+        ws = self.reducer.comm.world_size
+        return self.reducer.can_shard and 128 % ws == 0
+
+    def set_shard_fc(self, on: bool = True) -> None:
+        """Shard the fc1 weight's optimizer update over the ranks: its gradient is
+        reduce-scattered (GPU; the gloo CPU path all-reduces it), each rank updates its
+        128 / world_size rows and the updated rows are all-gathered (bf16 rows on the GPU,
+        fp32 rows on the CPU).  Optimizer state of the other rows is not kept current:
+        ``sync_master`` gathers it (checkpoints)."""
+        if self.gpu is not None:
+            self.gpu.set_shard_fc(on)
+            return
+        if not on:
+            self.sync_master()
+            self.reducer.clear_shard()
+            return
+        ws = self.reducer.comm.world_size
+        self.reducer.set_shard(0, self.arena.spec.offset("fc1.weight"), 128 // ws * 9216)
+
+    def sync_master(self) -> None:
+        """Make the fp32 master weights and optimizer state whole on every rank (a no-op
+        unless an update is sharded; collective then: every rank calls it)."""
+        if self.gpu is not None:
+            if hasattr(self.gpu, "sync_master"):
+                self.gpu.sync_master()
+            return
+        sh = getattr(self.reducer, "shard", None)
+        if sh is not None:
+            _, start, count = sh
+            n = count * self.reducer.comm.world_size
+            for buf in self.optimizer.state_buffers().values():
+                self.reducer.gather(buf[start:start + n])
+
     def run_steps(self, n: int, bsz: Optional[int] = None) -> None:
         """Run ``n`` full steps from the current counter (bench helper; GPU only)."""
         self.gpu.train_steps(bsz or self.batch_size, n)

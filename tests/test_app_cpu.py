@@ -122,3 +122,28 @@ def test_launch_mode_matches_spawn(tmp_path, explicit_init):
     sb = torch.load(d2 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)["state_dict"]
     for k in sa:   # torchrun sets OMP_NUM_THREADS=1: CPU GEMM sums may differ in the last ulp
         assert torch.allclose(sa[k], sb[k], atol=1e-6, rtol=0), k
+
+
+@pytest.mark.slow
+def test_cnn_sharded_fc1_update_matches_replicated_cpu(tmp_path):
+    """--shard-fc on the gloo CPU path (world size 2): each rank updates its 64 rows of fc1
+    and the rows are all-gathered; the full state is gathered before rank 0 saves.  The
+    checkpoint (parameters and momentum) is bit-identical to the replicated run's, and it
+    resumes at world size 1."""
+    d1, d2 = tmp_path / "rep", tmp_path / "shard"
+    d1.mkdir()
+    d2.mkdir()
+    common = ["--epochs", "1", "--synthetic-size", "512", "--world-size", "2", "--arch", "cnn",
+              "--optimizer", "sgd", "--lr", "0.05", "--batch-size", "128", "--seed", "4"]
+    run_cli(common, d1)
+    out = run_cli(common + ["--shard-fc"], d2)
+    assert len([l for l in out.splitlines() if EPOCH_RE.match(l)]) == 2
+    a = torch.load(d1 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)
+    b = torch.load(d2 / "checkpoints" / "checkpoint_0.pth.tar", weights_only=True)
+    for k in a["state_dict"]:
+        assert torch.equal(a["state_dict"][k], b["state_dict"][k]), k
+    for i, st in a["optimizer"]["state"].items():
+        assert torch.equal(st["momentum_buffer"], b["optimizer"]["state"][i]["momentum_buffer"]), i
+    out = run_cli(["--arch", "cnn", "--optimizer", "sgd", "--evaluate", "--resume",
+                   str(d2 / "checkpoints" / "checkpoint_0.pth.tar")], d2)
+    assert re.search(r"^test loss: \d+\.\d{6}, test acc: \d+\.\d{2}%\.$", out, re.M)

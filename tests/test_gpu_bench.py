@@ -51,7 +51,8 @@ def test_bench_transport_calibration(gpu):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     cal = d["config"]["transport_calibration_ms_per_step"]
-    assert set(cal) == {"xgmi", "rccl", "rccl-nocarry", "rccl-side", "rccl-early"}, cal
+    assert set(cal) == {"xgmi", "rccl", "rccl-nocarry", "rccl-side", "rccl-early",
+                        "rccl-zero"}, cal
     assert d["config"]["grad_transport"] == min(cal, key=cal.get)
     # what the data plane saw: a 1-rank RCCL communicator, no xGMI peer to map
     assert d["comm"]["rccl_comm_count"] == 1

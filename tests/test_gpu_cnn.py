@@ -36,6 +36,44 @@ def _program(B, opt="sgd", lr=0.0, graphs=False, n=600, seed=0):
     return prog, train, test
 
 
+class _RoundFwd(torch.autograd.Function):
+    """bf16 rounding in the forward, gradient passed through unchanged."""
+    @staticmethod
+    def forward(ctx, t):
+        return bf(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    """Identity in the forward, bf16 rounding of the gradient in the backward."""
+    @staticmethod
+    def forward(ctx, t):
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return bf(g)
+
+
+def bf16_mirrored_forward(p, x):
+    """The CNN forward with the kernel chain's bf16 rounding points (csrc/kernels/cnn_fwd.hip,
+    cnn_bwd.hip, docs/kernels.md): x, conv1 / conv2 / fc1 weights, a1 and the pooled features
+    are bf16 operands; dh (fc1 pre-activation grad, stored bf16 by cnn_head), dpool (bf16
+    from fc1_bwd's dX tiles) and da1 (the conv2 dgrad after relu', the bf16 A operand of the
+    conv1 weight-gradient MFMA) are rounded in the backward.  fp32 everywhere else."""
+    fr, gr = _RoundFwd.apply, _RoundGrad.apply
+    B = x.shape[0]
+    h = fr(x.reshape(B, 1, 28, 28))
+    a1 = fr(F.relu(gr(F.conv2d(h, fr(p["conv1.weight"]), p["conv1.bias"]))))
+    z2 = F.relu(F.conv2d(a1, fr(p["conv2.weight"]), p["conv2.bias"]))
+    pool = gr(fr(F.max_pool2d(z2, 2)))
+    h = F.relu(gr(F.linear(torch.flatten(pool, 1), fr(p["fc1.weight"]), p["fc1.bias"])))
+    return F.linear(h, p["fc2.weight"], p["fc2.bias"])
+
+
 def _torch_params(prog):
     return prog.arena.torch_tensors(prog.arena.params)
 
@@ -165,6 +203,15 @@ def test_cnn_step_gradients_match_autograd(gpu, B):
     for name, leaf in leaves.items():
         r = rel(got[name], leaf.grad)
         assert r < (1.2e-1 if name.startswith("conv") else 5e-2), (name, r)
+    # the same step in fp32 autograd with the kernels' bf16 rounding points mirrored
+    # (operands rounded in the forward, dh / dpool / da1 rounded in the backward): only fp32
+    # summation order and rare max-pool / ReLU ties differ, so the bound is tight
+    mleaves = {k: v.clone().requires_grad_() for k, v in tp.items()}
+    mloss = F.cross_entropy(bf16_mirrored_forward(mleaves, x), train.labels[sel])
+    mloss.backward()
+    for name, leaf in mleaves.items():
+        r = rel(got[name], leaf.grad)
+        assert r < (1e-2 if name.startswith("conv") else 3e-3), (name, r)
     m = prog.metrics.buf[0:3].cpu()
     assert abs(m[0].item() / B - loss.item()) < 2e-2 * max(1.0, loss.item())
     assert m[2].item() == B

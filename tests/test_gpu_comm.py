@@ -74,7 +74,7 @@ def test_grad_reducer_grouped_all_ready(gpu):
     comm.close()
 
 
-@pytest.mark.parametrize("carry", ["carry", "nocarry", "side", "early"])
+@pytest.mark.parametrize("carry", ["carry", "nocarry", "side", "early", "zero"])
 @pytest.mark.parametrize("B", [256, 32])
 def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
     """The world_size > 1 step structure (unfused conv reduction, grouped RCCL all-reduce of
@@ -95,6 +95,8 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
         p.gpu.fc_carry = carry not in ("nocarry", "early")
         p.gpu.fc_side = carry == "side"
         p.gpu.fc_early = carry == "early"
+        if force and carry == "zero":
+            p.gpu.set_shard_fc(True)           # 1 rank: the shard is all 128 rows
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         p.train_epoch()

@@ -4,6 +4,7 @@ set -o pipefail
 O=gpurun_out/r4a
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_cnn.py -x -v -k gradients_match --timeout 120 --timeout-method thread > $O/grad_test.log 2>&1
 : > $O/warm.jsonl
 for W in 5 50 500 5; do
   timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup $W >> $O/warm.jsonl 2>> $O/bench.err || exit 1
@@ -17,4 +18,5 @@ d=$O/trace_f32
 timeout -k 10 180 rocprofv3 --kernel-trace -d $d -o run -- python3 bench.py --dtype fp32 --steps 200 --warmup 30 > /dev/null 2>&1 || exit 1
 python tools/rocpd_summary.py $(ls $d/*.db) --title "in-step kernels, bench.py --dtype fp32 B=256, 200 steps" --steps 150 > $O/trace_f32.md && rm -rf $d
 rm -rf gpurun_out/pmc
+timeout -k 10 600 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_comm.py tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread > $O/new_tests.log 2>&1
 echo done
