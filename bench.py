@@ -36,7 +36,7 @@ import torch
 
 # The reference's own training loop with the CNN swapped in, PyTorch eager + DDP/RCCL on one
 # MI355X (tools/reference_eager.py, DataLoader with 4 workers, fp32, SGD momentum, batch 256;
-# profiles/reference_eager_n1.jsonl).  For N GPUs the baseline is taken as N x this value,
+# profiles/archive/r1_r2/reference_eager_n1.jsonl).  For N GPUs the baseline is taken as N x this value,
 # i.e. perfect weak scaling of the reference.
 REFERENCE_CNN_IMG_S_1GPU = 135369.5
 REFERENCE_LINEAR_IMG_S_1GPU = 221060.4
@@ -319,10 +319,8 @@ def main():
             prog.reducer = red
             prog.gpu.reducer = red
             prog.gpu.use_graphs = bool(a.graphs) and red.capturable
-            if hasattr(prog.gpu, "fc_carry"):
-                prog.gpu.fc_carry = carry not in ("nocarry", "early")
-                prog.gpu.fc_side = carry == "side"
-                prog.gpu.fc_early = carry == "early"
+            if hasattr(prog.gpu, "set_rccl_mode"):
+                prog.gpu.set_rccl_mode(carry, invalidate=False)
             prog.gpu.invalidate_graphs()
             if shardable and (carry == "zero" or os.environ.get("PDM_SHARD_FC") == "1") and \
                     red.active and prog.gpu.shard_supported():
@@ -336,21 +334,22 @@ def main():
                 prog.gpu.prepare(tail, sizes=(1,))
 
         # candidate step structures: every transport, and for RCCL the fc-update placement
-        # (cnn_step.CnnStep.fc_carry / fc_side: carried past the next cnn_fwd, one grouped
-        # launch, or on a side stream) unless PDM_FC_CARRY forces it
+        # (cnn_step.CnnStep: fc_carry = carried past the next cnn_fwd, nocarry = one grouped
+        # launch, fc_side = on a side stream, fc_early = all-reduce issued during the conv
+        # backward, zero = fc1 update sharded over the ranks) unless PDM_RCCL_MODE forces one
         cands = []
+        forced = os.environ.get("PDM_RCCL_MODE")
+        modes = ("carry", "nocarry", "side", "early", "zero")
+        if forced is not None and forced not in modes:
+            raise SystemExit(f"PDM_RCCL_MODE={forced!r}: choose from {modes}")
         for name, red in reducers.items():
-            if name == "rccl" and model == "cnn" and os.environ.get("PDM_FC_CARRY") is None:
-                cands += [("rccl", red, "carry"), ("rccl-nocarry", red, "nocarry"),
-                          ("rccl-side", red, "side"), ("rccl-early", red, "early")]
-                if shardable and prog.gpu.shard_supported(red):
-                    # fc1 optimizer-state sharding: reduce-scatter + sharded update + bf16
-                    # all-gather (CnnStep.set_shard_fc)
-                    cands.append(("rccl-zero", red, "zero"))
+            if name == "rccl" and model == "cnn":
+                ok = [m for m in modes if m != "zero" or
+                      (shardable and prog.gpu.shard_supported(red))]
+                for m in ([forced] if forced in ok else ok):
+                    cands.append(("rccl" if m == "carry" else f"rccl-{m}", red, m))
             else:
-                env = os.environ.get("PDM_FC_CARRY", "1") != "0"
-                side = os.environ.get("PDM_FC_SIDE", "0") == "1"
-                cands.append((name, red, "side" if side and env else ("carry" if env else "nocarry")))
+                cands.append((name, red, "carry"))
 
         opt.sync_hyperparams()
         next_epoch()

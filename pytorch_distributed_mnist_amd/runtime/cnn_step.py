@@ -176,23 +176,19 @@ class CnnStep(GpuStepBase):
         self.keep_grads = os.environ.get("PDM_KEEP_GRADS", "0") == "1"
         self.phase_period = 2 if self._wt_double_on() else 1
         self._fused = {}
-        # RCCL data plane: defer the fc-bucket update past the next step's cnn_fwd so the
-        # 4.7 MB all-reduce overlaps it (True), or reduce both buckets in one grouped RCCL
-        # launch and update every parameter in one optimizer launch (False: fewer launches
-        # when the transfer is short).  bench.py calibrates both; PDM_FC_CARRY=0/1 forces.
-        env = os.environ.get("PDM_FC_CARRY")
-        self.fc_carry = True if env is None else env != "0"
-        # ... or (fc_side, with fc_carry) run the fc-bucket update on a side stream as soon as
-        # its all-reduce lands, beside the conv update and the next cnn_fwd; the next fc1_fwd
-        # waits for it.  Worth it when those kernels leave CUs idle (small per-rank batches:
-        # cnn_fwd_band is 192 workgroups at B = 32 / 64); bench.py calibrates it as well.
-        self.fc_side = os.environ.get("PDM_FC_SIDE", "0") == "1"
-        # ... or (fc_early) issue the fc bucket's all-reduce right after fc1_bwd, so it runs
-        # during the conv backward, as DDP's Reducer does during loss.backward()
-        # (multi_proc_single_gpu.py:91).  At small per-rank batches cnn_bwd_band leaves CUs
-        # free for RCCL's kernel (B = 32: 192 workgroups on 256 CUs); at B = 256 cnn_bwd takes
-        # every CU and the collective waits for it.  bench.py calibrates it as well.
-        self.fc_early = os.environ.get("PDM_FC_EARLY", "0") == "1"
+        # RCCL data plane: where the fc bucket's all-reduce and update go (RCCL_MODES;
+        # bench.py calibrates every mode on the real step, PDM_RCCL_MODE picks one):
+        #  carry   defer the fc-bucket update past the next step's cnn_fwd, so the 4.7 MB
+        #          all-reduce overlaps that forward (it only needs the conv weights)
+        #  nocarry both buckets in one grouped RCCL launch, one optimizer launch (fewer
+        #          launches when the transfer is short)
+        #  side    the fc update on a side stream as soon as its all-reduce lands, beside the
+        #          conv update and the next cnn_fwd (small per-rank batches leave CUs idle)
+        #  early   the fc all-reduce issued right after fc1_bwd, during the conv backward, as
+        #          DDP's Reducer does during loss.backward() (multi_proc_single_gpu.py:91); at
+        #          small batches cnn_bwd_band leaves CUs free for RCCL's kernel (B = 32: 192
+        #          workgroups on 256 CUs), at B = 256 the collective waits for cnn_bwd
+        self.set_rccl_mode(os.environ.get("PDM_RCCL_MODE", "carry"), invalidate=False)
         # world_size > 1: optimizer-state sharding of the fc1 weight (set_shard_fc): its
         # gradient is reduce-scattered instead of all-reduced, each rank updates its
         # 128 / world_size rows (fp32 master, momentum, bf16 W1 rows) and the bf16 W1 rows are
@@ -205,6 +201,20 @@ class CnnStep(GpuStepBase):
         self._side_ev = None
         self.refresh_shadows()
         self._poison_unkept_grads()
+
+    RCCL_MODES = ("carry", "nocarry", "side", "early")
+
+    def set_rccl_mode(self, mode: str, invalidate: bool = True) -> None:
+        """Step structure of the fc bucket on the RCCL data plane (see __init__)."""
+        if mode == "zero":             # bench.py's name for carry + set_shard_fc(True)
+            mode = "carry"
+        if mode not in self.RCCL_MODES:
+            raise ValueError(f"RCCL step mode {mode!r}: choose from {self.RCCL_MODES}")
+        self.fc_carry = mode in ("carry", "side")
+        self.fc_side = mode == "side"
+        self.fc_early = mode == "early"
+        if invalidate:
+            self.invalidate_graphs()
 
     # -- fc1 optimizer-state sharding --------------------------------------------------------
     def shard_supported(self, reducer=None) -> bool:

@@ -92,9 +92,7 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
                                 momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=force,
                                 transport="rccl")
         assert p.gpu.fuse_conv_reduce == (not force)
-        p.gpu.fc_carry = carry not in ("nocarry", "early")
-        p.gpu.fc_side = carry == "side"
-        p.gpu.fc_early = carry == "early"
+        p.gpu.set_rccl_mode(carry)
         if force and carry == "zero":
             p.gpu.set_shard_fc(True)           # 1 rank: the shard is all 128 rows
         p.optimizer.sync_hyperparams()

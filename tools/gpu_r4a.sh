@@ -1,10 +1,11 @@
-# Round 4 probe: warm-up ramp of the driver's 20-step window, PMC tables (B=256 bf16,
-# B=32 bf16 through the N>1 chain, fp32 B=256) and an in-step trace of the fp32 bench.
+# Round 4 probe: new GPU tests, warm-up ramp of the driver's 20-step window, PMC tables
+# (B=256 bf16, B=32 bf16 through the N>1 chain, fp32 B=256), an in-step trace of the fp32
+# bench and the rccl-early overlap trace at B=32.
 set -o pipefail
 O=gpurun_out/r4a
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_cnn.py -x -v -k gradients_match --timeout 120 --timeout-method thread > $O/grad_test.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_cnn.py tests/test_gpu_shard.py tests/test_gpu_comm.py tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread > $O/new_tests.log 2>&1 || exit 1
 : > $O/warm.jsonl
 for W in 5 50 500 5; do
   timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup $W >> $O/warm.jsonl 2>> $O/bench.err || exit 1
@@ -17,6 +18,9 @@ cp gpurun_out/pmc/*.md $O/
 d=$O/trace_f32
 timeout -k 10 180 rocprofv3 --kernel-trace -d $d -o run -- python3 bench.py --dtype fp32 --steps 200 --warmup 30 > /dev/null 2>&1 || exit 1
 python tools/rocpd_summary.py $(ls $d/*.db) --title "in-step kernels, bench.py --dtype fp32 B=256, 200 steps" --steps 150 > $O/trace_f32.md && rm -rf $d
-rm -rf gpurun_out/pmc
-timeout -k 10 600 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_comm.py tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread > $O/new_tests.log 2>&1
+d=$O/trace_early32
+PDM_FORCE_COMM=1 PDM_COMM=rccl PDM_RCCL_MODE=early timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --scaling weak --batch-per-rank 32 --steps 200 --warmup 30 > $O/early32.json 2>&1 || exit 1
+python tools/overlap.py $d --a 'nccl|rccl|Nccl|Rccl' --b cnn_bwd > $O/overlap_early32.txt 2>&1
+python tools/pmc_table.py --trace $d $d > /dev/null 2>&1
+rm -rf gpurun_out/pmc $d/*.csv.gz
 echo done
