@@ -660,7 +660,7 @@ int64_t cnn_bwd_nblk(int64_t B, int64_t ipb, int64_t bands) { return conv_blocks
 void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr, int64_t bfull,
              int64_t B, at::Tensor w1, at::Tensor b1, at::Tensor w2, at::Tensor b2,
              at::Tensor pool, c10::optional<at::Tensor> pmask, c10::optional<at::Tensor> a1g,
-             c10::optional<at::Tensor> xng, at::Tensor ylab, int64_t spe) {
+             c10::optional<at::Tensor> xng, at::Tensor ylab, int64_t spe, bool x3) {
   c10::DeviceGuard g(images.device());
   need(images, at::kByte, "images");
   need(labels, at::kInt, "labels");
@@ -694,7 +694,7 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
                  w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                  pool.data_ptr<float>(), train ? pmask->data_ptr<uint8_t>() : nullptr,
                  train ? a1g->data_ptr<float>() : nullptr, train ? xng->data_ptr<float>() : nullptr,
-                 ylab.data_ptr<int32_t>(), cur_stream(images));
+                 ylab.data_ptr<int32_t>(), x3, cur_stream(images));
 }
 
 void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int64_t splitk) {
@@ -737,7 +737,7 @@ void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int
 }
 
 void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor pmask, at::Tensor w2,
-                  int64_t B, at::Tensor slab, int64_t ipb) {
+                  int64_t B, at::Tensor slab, int64_t ipb, bool x3) {
   c10::DeviceGuard g(a1g.device());
   TORCH_CHECK(B >= 1 && ipb >= 1, "B and ipb must be >= 1");
   need_min(a1g, at::kFloat, B * 676 * 32, "a1g");
@@ -750,7 +750,7 @@ void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor p
            "conv slab");
   launch_f32_conv_bwd(a1g.data_ptr<float>(), xng.data_ptr<float>(), dpool.data_ptr<float>(),
                       pmask.data_ptr<uint8_t>(), w2.data_ptr<float>(), (int)B, (int)ipb,
-                      slab.data_ptr<float>(), cur_stream(a1g));
+                      slab.data_ptr<float>(), x3, cur_stream(a1g));
 }
 
 // Upload an instantiated hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device
@@ -829,11 +829,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_reduce", &conv_reduce);
   m.def("f32_fwd", &f32_fwd, py::arg("images"), py::arg("labels"), py::arg("ctr"), py::arg("bfull"),
         py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"), py::arg("pool"),
-        py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"), py::arg("spe") = 0);
+        py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"), py::arg("spe") = 0,
+        py::arg("x3") = false);
   m.def("f32_fc1_fwd", &f32_fc1_fwd);
   m.def("f32_fc1_bwd", &f32_fc1_bwd);
   m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),
-        py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1);
+        py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1,
+        py::arg("x3") = false);
   m.def("f32_conv_bwd_nblk", [](int64_t B, int64_t ipb) {
     return (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb); }, py::arg("B"), py::arg("ipb") = 1);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);

@@ -169,6 +169,173 @@ __global__ __launch_bounds__(FT, 1) void f32_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------ f32 conv2 on the bf16 MFMA
+// Split-bf16 ("bf16x3") products: an fp32 operand x is carried as hi = bf16(x) and
+// lo = bf16(x - hi) (both round-to-nearest-even), |x - hi - lo| <= 2^-16 |x| (a normal x
+// whose hi / lo stay normal); a product x.y is taken as hi.hi + hi.lo + lo.hi on
+// v_mfma_f32_16x16x32_bf16 (exact bf16 products, fp32 accumulation), dropping lo.lo and the
+// operand remainders: relative error <= ~2^-15 per product, below fp32's 2^-24 ULP of a
+// partial sum only in the last few bits, far inside TF32's 2^-11 (what cuDNN uses for fp32
+// convolutions by default, torch.backends.cudnn.allow_tf32) -- at 3 MFMAs of 16 cycles per
+// 16x16x32 block against 8 f32-MFMAs of 32 cycles, 5.3x the fp32-MFMA rate.
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = to_bf16(v[j]);
+    lo[j] = to_bf16(v[j] - from_bf16(hi[j]));
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);   // small terms first
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+// f32x3_fwd: f32_fwd with conv2 on split-bf16 products.  conv1 stays exact fp32 on the VALU;
+// its output a1 is stored as hi / lo bf16 planes in the bf16 forward's swizzled LDS layout
+// (cnn_common.h a1_off), and conv2 runs cnn_fwd's tiling (16-row tiles = 4 pooled pixels x
+// 2x2 window, one tap = one K = 32 step) with the W2 fragments split once into registers.
+constexpr int XF_XS = 0;                          // fp32 x [784]
+constexpr int XF_WS = 3136;                       // fp32 w1 [288] | b1 [32] | b2 [64]
+constexpr int XF_AH = 4736;                       // bf16 a1 hi plane [676 px][64 B], swizzled
+constexpr int XF_AL = XF_AH + P1 * 64;            // bf16 a1 lo plane
+constexpr int XF_TOTAL = XF_AL + P1 * 64;         // 91264 B
+static_assert(XF_TOTAL <= 163840 && XF_AH % 128 == 0 && XF_AL % 128 == 0, "f32x3_fwd LDS");
+
+template <bool TRAIN>
+__global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
+    const uint8_t* __restrict__ images, const int32_t* __restrict__ labels, int64_t nrow,
+    const int64_t* __restrict__ ctr, const StepRows sr, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ pool, uint8_t* __restrict__ pmask, float* __restrict__ a1g,
+    float* __restrict__ xng, int32_t* __restrict__ ylab) {
+  __shared__ __attribute__((aligned(16))) char smem[XF_TOTAL];
+  float* xs = reinterpret_cast<float*>(smem + XF_XS);
+  float* ws = reinterpret_cast<float*>(smem + XF_WS);
+  const int img = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  // 0. small weights -> LDS, the image (epoch-buffer row ctr * bfull + img, or row img)
+  const int wt = tid - 256;
+  if (wt >= 0 && wt < 96) {
+    const float4 q = wt < 72 ? reinterpret_cast<const float4*>(w1)[wt]
+                     : wt < 80 ? reinterpret_cast<const float4*>(b1)[wt - 72]
+                               : reinterpret_cast<const float4*>(b2)[wt - 80];
+    reinterpret_cast<float4*>(ws)[wt] = q;
+  }
+  const int64_t row = min(ctr ? step_row(sr, nrow, *ctr, img) : (int64_t)img, nrow - 1);
+  if (tid < 196) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(images + row * 784)[tid];
+    const float4 x = make_float4(pdm_normalize(v & 0xff), pdm_normalize((v >> 8) & 0xff),
+                                 pdm_normalize((v >> 16) & 0xff), pdm_normalize(v >> 24));
+    reinterpret_cast<float4*>(xs)[tid] = x;
+    if (TRAIN) reinterpret_cast<float4*>(xng + (int64_t)img * 784)[tid] = x;
+  }
+  if (tid == 64) ylab[img] = labels[row];
+  // 1. this wave's conv2 B fragments, split: co = 32 nh + 16 j + i16, k = ci = 8 g .. 8 g + 7
+  // of tap t (W2 internal layout [co][ky][kx][ci]); in flight while conv1 runs
+  const int nh = wave & 1;
+  bf16x8 bh[9][2], bl[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4* src = reinterpret_cast<const float4*>(
+          w2 + ((int64_t)(nh * 32 + j * 16 + i16) * 9 + t) * 32 + 8 * g);
+      const float4 p0 = src[0], p1 = src[1];
+      const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+      split8(v, bh[t][j], bl[t][j]);
+    }
+  __syncthreads();
+  // 2. conv1 + bias + ReLU (exact fp32, VALU): thread = pixel, 8 channels per 16-B chunk of
+  // the hi / lo planes
+  for (int p = tid; p < P1; p += FT) {
+    const int y = p / H1, x = p - y * H1;
+    float xv[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) xv[t] = xs[(y + t / 3) * IMG + x + t % 3];
+#pragma unroll 1
+    for (int c8 = 0; c8 < C1 / 8; ++c8) {
+      float o[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int co = 8 * c8 + u;
+        float acc = ws[288 + co];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc = fmaf(ws[co * 9 + t], xv[t], acc);
+        o[u] = fmaxf(acc, 0.f);
+      }
+      bf16x8 h, l;
+      split8(o, h, l);
+      const int off = a1_off(y, x, 16 * c8);
+      *reinterpret_cast<bf16x8*>(smem + XF_AH + off) = h;
+      *reinterpret_cast<bf16x8*>(smem + XF_AL + off) = l;
+      if (TRAIN) {
+        float4* dst = reinterpret_cast<float4*>(a1g + ((int64_t)img * P1 + p) * C1 + 8 * c8);
+        dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+        dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
+    }
+  }
+  __syncthreads();
+  // 3. conv2 implicit GEMM (cnn_fwd's tiling): wave pair pr takes tiles [tt0, tt1), the wave
+  // its co half nh; lane (g, i16 = 4 q + s) reads pixel (2 py + (s >> 1) + ky,
+  // 2 px0 + 2 q + (s & 1) + kx), channels 8 g .. 8 g + 7 (swizzled chunk, per-lane constant)
+  const int q = i16 >> 2, s = i16 & 3;
+  const int lp = ((s >> 1) * H1 + 2 * q + (s & 1)) * 64;
+  int aoff[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+      aoff[ky * 3 + kx] = lp + (ky * H1 + kx) * 64 + ((g ^ ((2 * q + (s & 1) + kx) & 3)) << 4);
+  float b2r[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b2r[j] = ws[320 + nh * 32 + j * 16 + i16];
+  const int pr = wave >> 1;
+  const int tt0 = pr < 2 ? 10 * pr : 20 + 8 * (pr - 2), tt1 = tt0 + (pr < 2 ? 10 : 8);
+  for (int tt = tt0; tt < tt1; ++tt) {
+    const int py = tt / 3, px0 = 4 * (tt - py * 3);
+    const int tb = (2 * py * H1 + 2 * px0) * 64;
+    f32x4 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = f32x4{b2r[j], b2r[j], b2r[j], b2r[j]};
+#pragma unroll
+    for (int t3 = 0; t3 < 9; t3 += 3) {
+      bf16x8 ah[3], al[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        ah[u] = *reinterpret_cast<const bf16x8*>(smem + XF_AH + tb + aoff[t3 + u]);
+        al[u] = *reinterpret_cast<const bf16x8*>(smem + XF_AL + tb + aoff[t3 + u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[j] = mfma3(ah[u], al[u], bh[t3 + u][j], bl[t3 + u][j], acc[j]);
+    }
+    // epilogue (f32_fwd's): lane's 4 accumulators = the 2x2 window of pooled pixel px0 + g
+    const int pp = py * HP + px0 + g;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = nh * 32 + j * 16 + i16;
+      float m = acc[j][0];
+      uint32_t oh = 1u;
+#pragma unroll
+      for (int r = 1; r < 4; ++r) {
+        const bool gt = acc[j][r] > m;   // first position holding the max
+        m = gt ? acc[j][r] : m;
+        oh = gt ? (1u << r) : oh;
+      }
+      const bool pos = m > 0.f;
+      pool[(int64_t)img * FEAT + pp * C2 + co] = pos ? m : 0.f;
+      if (TRAIN) pmask[(int64_t)img * FEAT + pp * C2 + co] = (uint8_t)(pos ? 0x80u | oh : 0u);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ f32_fc1_fwd
 // part[s][row][n] = sum_{k in split s} pool[row][k] W1[n][k]; workgroup = 32 rows x 128 n of
 // one split, 4 waves x 32 n; K in LDS-staged chunks of 32 (rows padded to 36 floats: the
@@ -573,12 +740,238 @@ __global__ __launch_bounds__(FT, 1) void f32_conv_bwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------ f32x3_conv_bwd
+// f32_conv_bwd with both conv2 GEMMs on split-bf16 products (mfma3).  Workgroup = (image
+// group, row band of 4 conv2-output rows), 6 bands per image, as f32_conv_bwd; the operands
+// are staged as hi / lo bf16 planes (split once per element at staging):
+//   x     fp32 rows [d0, d0 + 8)                                            896 B
+//   a1    rows [d0, d0 + 6) x 26 px x 32 ci, a1_off layout (band-local row)  2 x 9984 B
+//   dz2   2 zero px + rows [d0 - 2, d0 + 7) x 26 px (cols 24, 25 zero: column -1 / -2 of a
+//         row wraps onto them) x 64 co, 128 B per px, 16-B chunk c at c ^ (px & 7)  2 x 30208 B
+//   W2^T  [tap][ci] rows of 64 co (128 B), chunk c at c ^ (ci & 7)              2 x 36864 B
+// dgrad: D[a1 px][ci] = sum_tap sum_co dz2[px - tap][co] W2[co][tap][ci] (A rows by
+// ds_read_b128, K = 64 co per tap = 2 k-steps), fused with relu'(a1) and the conv1
+// weight / bias gradient (the exact fp32 MFMA of f32_conv_bwd, A = the dgrad accumulator).
+// wgrad: D[co][tap, ci] = sum_px dz2[px][co] a1[px + tap][ci] over the band's 96 output
+// pixels (3 k-steps; both operands by ds_read_b64_tr_b16 column reads); wave w owns co tile
+// w & 3 and the 9 (tap, ci tile) columns 9 (w >> 2) ..; accumulators persist over the
+// workgroup's images.  One fp32 slab per workgroup, f32_conv_bwd's layout.
+constexpr int XB_XS = 0;
+constexpr int XB_AP = 6 * H1 * 64;                 // a1 plane (9984 B)
+constexpr int XB_AH = 1024;
+constexpr int XB_AL = XB_AH + XB_AP;
+constexpr int XB_DP = (2 + 9 * H1) * 128;          // dz2 plane (30208 B)
+constexpr int XB_DH = XB_AL + XB_AP;
+constexpr int XB_DL = XB_DH + XB_DP;
+constexpr int XB_WP = 9 * C1 * 128;                // W2^T plane (36864 B)
+constexpr int XB_WH = XB_DL + XB_DP;
+constexpr int XB_WL = XB_WH + XB_WP;
+constexpr int XB_TOTAL = XB_WL + XB_WP;            // 155136 B
+static_assert(XB_TOTAL <= 163840 && XB_AH % 128 == 0 && XB_DH % 128 == 0 && XB_WH % 128 == 0,
+              "f32x3_conv_bwd LDS");
+static_assert((8 * C2 + 8 * 512) * 4 <= 2 * XB_DP, "reduction scratch fits the dz2 planes");
+
+__device__ __forceinline__ int xdz_off(int zp, int chunk) { return zp * 128 + ((chunk ^ (zp & 7)) << 4); }
+__device__ __forceinline__ int xw_off(int tap, int ci, int chunk) {
+  return (tap * C1 + ci) * 128 + ((chunk ^ (ci & 7)) << 4);
+}
+
+__global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
+    const float* __restrict__ a1g, const float* __restrict__ xng, const float* __restrict__ dpool,
+    const uint8_t* __restrict__ pmask, const float* __restrict__ w2, int B, int ipb,
+    float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) char smem[XB_TOTAL];
+  float* xs = reinterpret_cast<float*>(smem + XB_XS);
+  const int grp = blockIdx.x / CB_S, band = blockIdx.x - grp * CB_S;
+  const int d0 = band * CB_R;
+  const int aown = band == CB_S - 1 ? CB_R + 2 : CB_R;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  float* out = slab + (int64_t)blockIdx.x * CNN_CONV_SLAB;
+  const int pr0 = band == 0 ? 0 : d0 / 2 - 1;
+  const int npr = d0 / 2 + CB_R / 2 - pr0;
+  const int npx = aown * H1, nmt = (npx + 15) / 16;
+  // W2^T hi / lo once per workgroup: item (tap, chunk, ci) gathers co 8 chunk .. + 7
+  for (int e = tid; e < 9 * 8 * C1; e += FT) {
+    const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = w2[(8 * c + u) * 288 + tap * 32 + ci];
+    bf16x8 h, l;
+    split8(v, h, l);
+    *reinterpret_cast<bf16x8*>(smem + XB_WH + xw_off(tap, ci, c)) = h;
+    *reinterpret_cast<bf16x8*>(smem + XB_WL + xw_off(tap, ci, c)) = l;
+  }
+  // wgrad: this wave's co tile and (tap, ci tile) columns; per-lane tr-read pieces
+  const int wmt = wave & 3, wn0 = 9 * (wave >> 2);
+  const int q = (lane >> 2) & 3, pq = lane & 3;
+  f32x4 wacc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) wacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float db2p = 0.f;
+  for (int ii = 0; ii < ipb; ++ii) {
+    const int img = grp * ipb + ii;
+    if (img >= B) break;                           // workgroup-uniform
+    __syncthreads();   // the previous image's reads of dz2 / a1 / x are done
+    // ---- staging: zero dz2 (both planes), x rows, a1 rows split
+    for (int i = tid; i < 2 * XB_DP / 16; i += FT)
+      reinterpret_cast<uint4*>(smem + XB_DH)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < (CB_R + 4) * IMG; i += FT) xs[i] = xng[(int64_t)img * 784 + d0 * IMG + i];
+    for (int i = tid; i < (CB_R + 2) * H1 * 4; i += FT) {
+      const int p = i >> 2, c = i & 3;
+      const float4* s4 = reinterpret_cast<const float4*>(
+          a1g + ((int64_t)img * P1 + d0 * H1 + p) * C1 + 8 * c);
+      const float4 u0 = s4[0], u1 = s4[1];
+      const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      bf16x8 h, l;
+      split8(v, h, l);
+      const int off = a1_off(p / H1, p % H1, 16 * c);
+      *reinterpret_cast<bf16x8*>(smem + XB_AH + off) = h;
+      *reinterpret_cast<bf16x8*>(smem + XB_AL + off) = l;
+    }
+    __syncthreads();
+    // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
+    for (int it = tid; it < npr * HP * C2; it += FT) {
+      const int pl = it >> 6, co = it & 63;
+      const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
+      const int gi = (py * HP + px) * C2 + co;
+      const uint8_t mk = pmask[(int64_t)img * FEAT + gi];
+      if (mk & 0x80) {
+        const float v = dpool[(int64_t)img * FEAT + gi];
+        const int sidx = __builtin_ctz((unsigned)mk & 0xf);
+        const int lr = 2 * py + (sidx >> 1) - (d0 - 2);
+        const int zp = 2 + lr * H1 + 2 * px + (sidx & 1);
+        const int o = xdz_off(zp, co >> 3) + 2 * (co & 7);
+        const bf16 h = to_bf16(v);
+        *reinterpret_cast<bf16*>(smem + XB_DH + o) = h;
+        *reinterpret_cast<bf16*>(smem + XB_DL + o) = to_bf16(v - from_bf16(h));
+        if (py >= d0 / 2) db2p += v;
+      }
+    }
+    __syncthreads();
+    // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
+    for (int mt = wave; mt < nmt; mt += 8) {
+      const int p = min(mt * 16 + i16, npx - 1);
+      const int y = p / H1, x = p - y * H1;
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 1
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const int zp = 2 + (y + 2 - ky) * H1 + x - kx;
+        bf16x8 ah[2], al[2], bh[2][2], bl[2][2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          ah[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DH + xdz_off(zp, 4 * kk + g));
+          al[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DL + xdz_off(zp, 4 * kk + g));
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const int wo = xw_off(tap, nt * 16 + i16, 4 * kk + g);
+            bh[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WH + wo);
+            bl[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WL + wo);
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma3(ah[kk], al[kk], bh[kk][nt], bl[kk][nt], acc[nt]);
+      }
+      float xb[4];
+      const int ctap = i16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = mt * 16 + 4 * g + r;
+        const int yy = pr / H1, xx = pr - yy * H1;
+        const bool valid = pr < npx;
+        xb[r] = !valid ? 0.f
+                : ctap < 9 ? xs[(yy + ctap / 3) * IMG + xx + ctap % 3]
+                : ctap == 9 ? 1.f : 0.f;
+        const int pc = min(pr, npx - 1);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          // relu'(a1): a1 >= 0, so a1 > 0 iff its hi or lo part is non-zero
+          const int o = a1_off(pc / H1, pc % H1, 2 * (nt * 16 + i16));
+          const unsigned short hb = *reinterpret_cast<const unsigned short*>(smem + XB_AH + o);
+          const unsigned short lb = *reinterpret_cast<const unsigned short*>(smem + XB_AL + o);
+          acc[nt][r] = (valid && (hb | lb) != 0) ? acc[nt][r] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
+    }
+    // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
+    // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
+    // the addresses of pixels col0 + q and col0 + 4 + q of that run, columns 4 pq .. 4 pq + 3
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int v = 4 * ks + g, r = v / 3, col0 = (v - 3 * r) * 8;
+      bf16x8 ah, al;
+      {
+        const int zp0 = 2 + (r + 2) * H1 + col0 + q, zp1 = zp0 + 4;
+        const int ch = 2 * wmt + (pq >> 1), bo = 8 * (pq & 1);
+        ah = cat_tr(lds_tr16(smem + XB_DH + xdz_off(zp0, ch) + bo),
+                    lds_tr16(smem + XB_DH + xdz_off(zp1, ch) + bo));
+        al = cat_tr(lds_tr16(smem + XB_DL + xdz_off(zp0, ch) + bo),
+                    lds_tr16(smem + XB_DL + xdz_off(zp1, ch) + bo));
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int nn = wn0 + j, tap = nn >> 1, ct = nn & 1;
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const int o0 = a1_off(r + ky, col0 + q + kx, 2 * (ct * 16 + 4 * pq));
+        const int o1 = a1_off(r + ky, col0 + 4 + q + kx, 2 * (ct * 16 + 4 * pq));
+        const bf16x8 bh = cat_tr(lds_tr16(smem + XB_AH + o0), lds_tr16(smem + XB_AH + o1));
+        const bf16x8 bl = cat_tr(lds_tr16(smem + XB_AL + o0), lds_tr16(smem + XB_AL + o1));
+        wacc[j] = mfma3(ah, al, bh, bl, wacc[j]);
+      }
+    }
+  }
+  __syncthreads();   // dz2 planes free: reduction scratch
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int nn = wn0 + j, tap = nn >> 1, ct = nn & 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      out[(wmt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16] = wacc[j][r];
+  }
+  float* red = reinterpret_cast<float*>(smem + XB_DH);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave * 512 + (nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
+  red[4096 + tid] = db2p;
+  __syncthreads();
+  if (tid < C2) {
+    float sacc = 0.f;
+    for (int w = 0; w < 8; ++w) sacc += red[4096 + w * 64 + tid];
+    out[SLB_DB2 + tid] = sacc;
+  } else if (tid >= 64 && tid < 64 + C1 * 10) {
+    const int e = tid - 64, ci = e / 10, tp = e - 10 * ci;
+    float sacc = 0.f;
+    for (int w = 0; w < 8; ++w) sacc += red[w * 512 + ci * 16 + tp];
+    if (tp < 9) out[SLB_DW1 + ci * 9 + tp] = sacc;
+    else out[SLB_DB1 + ci] = sacc;
+  }
+}
+
 }  // namespace
 
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
                     StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
-                    int32_t* ylab, hipStream_t st) {
+                    int32_t* ylab, bool x3, hipStream_t st) {
+  if (x3) {
+    if (a1g != nullptr)
+      f32x3_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2, pool,
+                                               pmask, a1g, xng, ylab);
+    else
+      f32x3_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2,
+                                                pool, pmask, a1g, xng, ylab);
+    return;
+  }
   if (a1g != nullptr)
     f32_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2, pool,
                                            pmask, a1g, xng, ylab);
@@ -604,7 +997,12 @@ int f32_conv_bwd_blocks(int B, int ipb) { return ((B + ipb - 1) / ipb) * CB_S; }
 
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
                          const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
-                         hipStream_t st) {
+                         bool x3, hipStream_t st) {
+  if (x3) {
+    f32x3_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(a1g, xng, dpool, pmask, w2,
+                                                                       B, ipb, slab);
+    return;
+  }
   f32_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(a1g, xng, dpool, pmask, w2, B,
                                                                    ipb, slab);
 }

@@ -73,6 +73,12 @@ class CnnStepF32(GpuStepBase):
                                           "fc2.bias")}
         self.G = {n: a.grad(n) for n in self.P}
         self.fuse_conv_reduce = not self.reducer.active
+        # conv2 products: "x3" = split-bf16 on the bf16 MFMA (hi.hi + hi.lo + lo.hi, fp32
+        # accumulation; cnn_f32.hip f32x3_*), "exact" = the fp32 MFMA (exact fp32 products)
+        mode = os.environ.get("PDM_F32_CONV", "exact")
+        if mode not in ("x3", "exact"):
+            raise ValueError(f"PDM_F32_CONV={mode!r}: x3 or exact")
+        self.conv_x3 = mode == "x3"
         if getattr(self.reducer, "streamed", False):
             # the persistent (streamed) xgmi collective is wired into the bf16 kernels' device
             # hand-off words; the fp32 program uses the transport's per-bucket launches
@@ -113,7 +119,8 @@ class CnnStepF32(GpuStepBase):
         ldt = -(-B // 32) * 32
         C.f32_fwd(self.ep_images.view(-1, 784), self.ep_labels, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
-                  self.pool, self.pmask, self.a1g, self.xng, self.ylab, spe=self.spe)
+                  self.pool, self.pmask, self.a1g, self.xng, self.ylab, spe=self.spe,
+                  x3=self.conv_x3)
         C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN)
         C.cnn_head(self.part, SPLITK_TRAIN, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                    self.ylab, True, None, None, ldt, self.head_slab, self.metrics.train_view(),
@@ -125,7 +132,7 @@ class CnnStepF32(GpuStepBase):
         red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
         ipb = conv_ipb(B)
         C.f32_conv_bwd(self.a1g, self.xng, self.dpool, self.pmask, P["conv2.weight"], B,
-                       self.conv_slab, ipb)
+                       self.conv_slab, ipb, x3=self.conv_x3)
         nblk = C.f32_conv_bwd_nblk(B, ipb)
         if self.fuse_conv_reduce:
             self.launch_optimizer(self._fused_segments(nblk))
@@ -144,7 +151,7 @@ class CnnStepF32(GpuStepBase):
             se = splitk_eval(b)
             C.f32_fwd(self.test_images[s:s + b], self.test_labels[s:s + b], None, b, b,
                       P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
-                      self.pool, None, None, None, self.ylab)
+                      self.pool, None, None, None, self.ylab, x3=self.conv_x3)
             C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, b, se)
             C.cnn_head(self.part, se, b, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
                        False, None, None, 32, None, self.metrics.eval_view(), None, None)

@@ -56,13 +56,15 @@ def _fp64_grads_with_mask(prog, x, y, pmask, B):
     return dict(net.named_parameters()), out
 
 
+@pytest.mark.parametrize("conv", ["exact", "x3"])
 @pytest.mark.parametrize("B", [64, 37, 256])
-def test_f32_gradients_match_fp32_autograd(gpu, B):
+def test_f32_gradients_match_fp32_autograd(gpu, B, conv):
     """One training step with lr = 0: the gradient arena holds the step's gradients (the fused
     optimizer writes the reduced conv gradients back).  Compared per parameter with fp64
     autograd of the same step (max-pool routed as the kernel routed it): <= 1e-4 relative,
     fp32 summation-order noise; and with fp32 autograd (torch's own routing)."""
     prog, train, _ = _program(B, n=max(2 * B, 300))
+    prog.gpu.conv_x3 = conv == "x3"
     idx = distributed_indices(len(train), 1, 0, 0)
     prog.set_train_indices(idx)
     net = _reference_net(prog)

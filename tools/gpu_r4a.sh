@@ -5,6 +5,9 @@ set -o pipefail
 O=gpurun_out/r4a
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_cnn_f32.py -v --timeout 300 --timeout-method thread > $O/f32_tests.log 2>&1
+rc=$?; [ $rc -le 1 ] || exit $rc          # test failures are data; anything else ends the call
+timeout -k 10 240 env PDM_F32_CONV=x3 python bench.py --dtype fp32 > $O/f32x3_bench.json 2>> $O/bench.err || exit 1
 timeout -k 10 900 python -u -m pytest tests/test_gpu_cnn.py tests/test_gpu_shard.py tests/test_gpu_comm.py tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread > $O/new_tests.log 2>&1 || exit 1
 : > $O/warm.jsonl
 for W in 5 50 500 5; do
