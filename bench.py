@@ -415,10 +415,13 @@ def main():
             raise RuntimeError("non-finite parameters after the benchmark")
         ms = elapsed / a.steps * 1e3
         sharded = bool(getattr(prog.gpu, "shard_fc", False))
+        conv2 = ("split-bf16 (hi.hi + hi.lo + lo.hi), fp32 accumulation"
+                 if getattr(prog.gpu, "conv_x3", False) else
+                 "fp32 MFMA" if dtype == "fp32" else "bf16 MFMA, fp32 accumulation")
         if shardable:
             prog.gpu.set_shard_fc(False)
         return {"B": B, "global_batch": B * ws, "elapsed": elapsed, "ms": ms, "shard_fc": sharded,
-                "value": imgs * ws / elapsed, "images": imgs * ws, "tail": tail,
+                "value": imgs * ws / elapsed, "images": imgs * ws, "tail": tail, "conv2": conv2,
                 "epoch_steps": spe, "transport": best,
                 "calib": {k: round(v, 5) for k, v in calib.items()},
                 "graphs": bool(prog.gpu.use_graphs), "epoch_boundaries_timed": boundaries}
@@ -463,6 +466,7 @@ def main():
                        "epoch_boundaries_timed": m["epoch_boundaries_timed"],
                        "epoch_steps": m["epoch_steps"], "tail_batch_per_rank": m["tail"],
                        "fc1_update_sharded": m["shard_fc"],
+                       "conv2_products": m["conv2"],
                        "images_timed": m["images"]},
             "value_semantics": (
                 "weak scaling: images/sec of the whole node at a fixed per-rank batch; timed "

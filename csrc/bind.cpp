@@ -316,7 +316,7 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
     s.tfrag = (t.size() > 7 && !t[7].is_none() && t[7].cast<bool>()) ? 1 : 0;
     s.sfrag = (t.size() > 8 && !t[8].is_none() && t[8].cast<bool>()) ? 1 : 0;
     if (s.sfrag)
-      TORCH_CHECK(s.shadow != nullptr && s.slab == nullptr && s.rows % 16 == 0 && s.cols % 32 == 0,
+      TORCH_CHECK(s.shadow != nullptr && s.rows % 16 == 0 && s.cols % 32 == 0,
                   "a fragment-major shadow needs a 2-D segment with rows % 16 == 0 and cols % 32 == 0 "
                   "(a row shard of it starts on a 16-row fragment boundary)");
     if (s.tfrag)

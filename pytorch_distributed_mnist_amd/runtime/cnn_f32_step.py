@@ -1,8 +1,10 @@
 """CNN fp32 GPU step program (``--arch cnn --dtype fp32``): the reference's precision.
 
 The reference trains in fp32 (``multi_proc_single_gpu.py:185-191``).  Same chain as the bf16
-program (``cnn_step.py``), on the fp32 matrix cores (``csrc/kernels/cnn_f32.hip``,
-``v_mfma_f32_16x16x4_f32``), reading the fp32 master weights directly (no bf16 copies):
+program (``cnn_step.py``) with fp32 activations, gradients and weights
+(``csrc/kernels/cnn_f32.hip``).  The conv2 GEMMs run as split-bf16 products on the bf16
+MFMA (``conv_x3``, see below) or exactly on the fp32 MFMA (``v_mfma_f32_16x16x4_f32``);
+fc1 runs on the fp32 MFMA:
 
   f32_fwd      gather-free epoch buffer row, normalise, conv1 + ReLU, conv2 + ReLU + maxpool
                -> pool, mask; a1 and the normalised x for the backward
@@ -73,9 +75,13 @@ class CnnStepF32(GpuStepBase):
                                           "fc2.bias")}
         self.G = {n: a.grad(n) for n in self.P}
         self.fuse_conv_reduce = not self.reducer.active
-        # conv2 products: "x3" = split-bf16 on the bf16 MFMA (hi.hi + hi.lo + lo.hi, fp32
-        # accumulation; cnn_f32.hip f32x3_*), "exact" = the fp32 MFMA (exact fp32 products)
-        mode = os.environ.get("PDM_F32_CONV", "exact")
+        # conv2 products (the step's FLOPs): "x3" (default) = split-bf16 on the bf16 MFMA
+        # (hi.hi + hi.lo + lo.hi, fp32 accumulation; cnn_f32.hip f32x3_*): 4.5e-6 relative
+        # error on a conv2 output against fp64, where exact fp32 gives 1.6e-7 and TF32 --
+        # cuDNN's default for fp32 convolutions -- 2.9e-4 (tests/test_split_bf16.py); the
+        # step's gradients stay within 1e-4 of fp64 (tests/test_gpu_cnn_f32.py).
+        # "exact" = the fp32 MFMA (exact fp32 products, 1.9x the step time).
+        mode = os.environ.get("PDM_F32_CONV", "x3")
         if mode not in ("x3", "exact"):
             raise ValueError(f"PDM_F32_CONV={mode!r}: x3 or exact")
         self.conv_x3 = mode == "x3"
