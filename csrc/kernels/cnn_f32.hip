@@ -851,31 +851,30 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
       }
     }
     __syncthreads();
-    // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
-    for (int mt = wave; mt < nmt; mt += 8) {
+    // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad:
+    // units (pixel tile mt, ci tile nt), unit u = 2 mt + nt on wave u % 8 (7 or 10 tiles x 2
+    // = 14 or 20 units: at most 3 per wave, where whole tiles left two waves with twice the
+    // work of the others)
+    for (int u = wave; u < 2 * nmt; u += 8) {
+      const int mt = u >> 1, nt = u & 1;
       const int p = min(mt * 16 + i16, npx - 1);
       const int y = p / H1, x = p - y * H1;
-      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
       for (int tap = 0; tap < 9; ++tap) {
         const int ky = tap / 3, kx = tap - 3 * ky;
         const int zp = 2 + (y + 2 - ky) * H1 + x - kx;
-        bf16x8 ah[2], al[2], bh[2][2], bl[2][2];
+        bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           ah[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DH + xdz_off(zp, 4 * kk + g));
           al[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DL + xdz_off(zp, 4 * kk + g));
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const int wo = xw_off(tap, nt * 16 + i16, 4 * kk + g);
-            bh[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WH + wo);
-            bl[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WL + wo);
-          }
+          const int wo = xw_off(tap, nt * 16 + i16, 4 * kk + g);
+          bh[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_WH + wo);
+          bl[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_WL + wo);
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma3(ah[kk], al[kk], bh[kk][nt], bl[kk][nt], acc[nt]);
+        for (int kk = 0; kk < 2; ++kk) acc = mfma3(ah[kk], al[kk], bh[kk], bl[kk], acc);
       }
       float xb[4];
       const int ctap = i16;
@@ -888,19 +887,19 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
                 : ctap < 9 ? xs[(yy + ctap / 3) * IMG + xx + ctap % 3]
                 : ctap == 9 ? 1.f : 0.f;
         const int pc = min(pr, npx - 1);
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          // relu'(a1): a1 >= 0, so a1 > 0 iff its hi or lo part is non-zero
-          const int o = a1_off(pc / H1, pc % H1, 2 * (nt * 16 + i16));
-          const unsigned short hb = *reinterpret_cast<const unsigned short*>(smem + XB_AH + o);
-          const unsigned short lb = *reinterpret_cast<const unsigned short*>(smem + XB_AL + o);
-          acc[nt][r] = (valid && (hb | lb) != 0) ? acc[nt][r] : 0.f;
-        }
+        // relu'(a1): a1 >= 0, so a1 > 0 iff its hi or lo part is non-zero
+        const int o = a1_off(pc / H1, pc % H1, 2 * (nt * 16 + i16));
+        const unsigned short hb = *reinterpret_cast<const unsigned short*>(smem + XB_AH + o);
+        const unsigned short lb = *reinterpret_cast<const unsigned short*>(smem + XB_AL + o);
+        acc[r] = (valid && (hb | lb) != 0) ? acc[r] : 0.f;
       }
+      if (nt == 0) {                  // wave-uniform
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < 4; ++r) acc1[0] = mfma4(acc[r], xb[r], acc1[0]);
+      } else {
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
+        for (int r = 0; r < 4; ++r) acc1[1] = mfma4(acc[r], xb[r], acc1[1]);
+      }
     }
     // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
     // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
