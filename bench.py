@@ -33,6 +33,7 @@ import sys
 import time
 
 import torch
+from pytorch_distributed_mnist_amd import knobs
 
 # The reference's own training loop with the CNN swapped in, PyTorch eager + DDP/RCCL on one
 # MI355X (tools/reference_eager.py, DataLoader with 4 workers, fp32, SGD momentum, batch 256;
@@ -133,7 +134,7 @@ def spawn_ranks(n: int, argv) -> int:
 
 def dry_run(a, rank: int, ws: int) -> None:
     import torch.distributed as dist
-    if os.environ.get("PDM_BENCH_FAIL_RANK") == str(rank):
+    if knobs.get("PDM_BENCH_FAIL_RANK") == str(rank):
         sys.exit(3)                 # fault injection (tests): this rank dies before rendezvous
     if ws > 1:
         dist.init_process_group("gloo", init_method="env://", world_size=ws, rank=rank)
@@ -145,7 +146,7 @@ def dry_run(a, rank: int, ws: int) -> None:
         total = 0.0
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": ws, "rank_sum": total,
-                          "launch": "spawned" if os.environ.get("PDM_BENCH_SPAWNED") else
+                          "launch": "spawned" if knobs.get("PDM_BENCH_SPAWNED") else
                           ("launcher" if ws > 1 else "single")}), flush=True)
 
 
@@ -160,6 +161,9 @@ def main():
     if a.dry_run:
         dry_run(a, rank, ws)
         return
+    if knobs.unknown() and rank == 0:
+        print(f"bench.py: warning: unknown PDM_* variables (typos?) {knobs.unknown()}",
+              file=sys.stderr, flush=True)
     from types import SimpleNamespace
 
     from pytorch_distributed_mnist_amd import parallel
@@ -174,12 +178,12 @@ def main():
     device = parallel.pick_device(local_rank, "cuda")
     # PDM_BENCH_BACKEND=gloo: rehearsal of the multi-rank flow on a single GPU (with
     # PDM_SHARE_DEVICE=1); the measured configuration is always nccl = RCCL
-    backend = os.environ.get("PDM_BENCH_BACKEND", "nccl")
+    backend = knobs.get("PDM_BENCH_BACKEND", "nccl")
     ctx = parallel.init_distributed(backend, "env://" if ws > 1 else None, ws, rank, local_rank,
                                     device, timeout_s=a.timeout, init_pg=ws > 1)
     # PDM_FORCE_COMM=1 at N=1: run the multi-GPU step structure (conv reduction, bucket
     # all-reduces through a 1-rank communicator) to price it without transfers
-    force_comm = os.environ.get("PDM_FORCE_COMM") == "1"
+    force_comm = knobs.get("PDM_FORCE_COMM") == "1"
     model = a.model
     spec = get_spec(model)
     parallel.verify_params_across_ranks(spec, rank, ws)
@@ -197,7 +201,7 @@ def main():
     # Gradient transports to choose from: with $PDM_COMM unset (auto) on the RCCL data plane
     # both the direct xGMI all-reduce and RCCL are built, and a short untimed calibration
     # run of the real step picks the faster one for this N and batch (agreed over ranks).
-    want = os.environ.get("PDM_COMM", "auto")
+    want = knobs.get("PDM_COMM", "auto")
     reducers = {}
     notes = []
     if (ws > 1 or force_comm) and want == "auto" and isinstance(comm, parallel.RcclComm):
@@ -252,7 +256,7 @@ def main():
                 orders.pop(e - 3, None)
             return orders[e]
 
-        dbg = os.environ.get("PDM_BENCH_DEBUG")
+        dbg = knobs.get("PDM_BENCH_DEBUG")
         marks = []
 
         def mark(what):
@@ -264,7 +268,7 @@ def main():
             prefetch.get(state["epoch"])          # queues the following epochs' orders
             idx = order(state["epoch"])
             nxt = order(state["epoch"] + 1) if \
-                os.environ.get("PDM_GATHER_AHEAD", "1") != "0" else None
+                knobs.get("PDM_GATHER_AHEAD", "1") != "0" else None
             mark("gather")
             prog.set_train_indices(idx, nxt)
             mark("begin_epoch")
@@ -322,7 +326,7 @@ def main():
             if hasattr(prog.gpu, "set_rccl_mode"):
                 prog.gpu.set_rccl_mode(carry, invalidate=False)
             prog.gpu.invalidate_graphs()
-            if shardable and (carry == "zero" or os.environ.get("PDM_SHARD_FC") == "1") and \
+            if shardable and (carry == "zero" or knobs.get("PDM_SHARD_FC") == "1") and \
                     red.active and prog.gpu.shard_supported():
                 prog.gpu.set_shard_fc(True)
 
@@ -338,7 +342,7 @@ def main():
         # launch, fc_side = on a side stream, fc_early = all-reduce issued during the conv
         # backward, zero = fc1 update sharded over the ranks) unless PDM_RCCL_MODE forces one
         cands = []
-        forced = os.environ.get("PDM_RCCL_MODE")
+        forced = knobs.get("PDM_RCCL_MODE")
         modes = ("carry", "nocarry", "side", "early", "zero")
         if forced is not None and forced not in modes:
             raise SystemExit(f"PDM_RCCL_MODE={forced!r}: choose from {modes}")
@@ -400,7 +404,7 @@ def main():
         # the W warmup steps run right before the timed window as usual.
         left = spe - state["step"]
         if a.steps >= 2 and left > a.steps // 2 + a.warmup and \
-                os.environ.get("PDM_BENCH_BOUNDARY", "1") != "0":
+                knobs.get("PDM_BENCH_BOUNDARY", "1") != "0":
             skip = left - a.steps // 2 - a.warmup
             sync("reposition")
             prog.gpu.skip_steps(skip)          # device data-step counter
@@ -476,9 +480,8 @@ def main():
                 "strong scaling: the reference's node batch 256 split over the ranks (S:174)"),
             "comm": comm_info,
             # every PDM_* environment knob this run saw (none set = the defaults)
-            "knobs": {k: v for k, v in sorted(os.environ.items())
-                      if k.startswith("PDM_") and k != "PDM_BENCH_SPAWNED"},
-            "launch": "spawned" if os.environ.get("PDM_BENCH_SPAWNED") else
+            "knobs": {k: v for k, v in knobs.active().items() if k != "PDM_BENCH_SPAWNED"},
+            "launch": "spawned" if knobs.get("PDM_BENCH_SPAWNED") else
                       ("launcher" if ws > 1 else "single"),
         }
         if main_mode == "weak" and "strong" in res:

@@ -21,6 +21,7 @@ import subprocess
 import sys
 import sysconfig
 from concurrent.futures import ThreadPoolExecutor
+from . import knobs
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "pytorch_distributed_mnist_amd")
@@ -63,16 +64,16 @@ def compile_flags(abi: int, inc):
              "-Wno-unused-result", "-Wno-deprecated-declarations",
              f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}"]
     flags += [f"-I{p}" for p in inc]
-    if os.environ.get("PDM_DEBUG_BOUNDS"):
+    if knobs.get("PDM_DEBUG_BOUNDS"):
         flags.append("-DPDM_DEBUG_BOUNDS=1")
-    if os.environ.get("PDM_STAMPS"):
+    if knobs.get("PDM_STAMPS"):
         flags.append("-DPDM_STAMPS=1")
-    if os.environ.get("PDM_DIAG_ROLES"):                   # fc1_bwd single-role launches
+    if knobs.get("PDM_DIAG_ROLES"):                   # fc1_bwd single-role launches
         flags.append("-DPDM_DIAG_ROLES=1")
     for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS", "PDM_NT"):   # tuning experiments (diagnostic builds)
         if os.environ.get(k):
             flags.append(f"-D{k}={int(os.environ[k])}")
-    if os.environ.get("PDM_HIPCC_FLAGS"):                  # compiler experiments (diagnostic builds)
+    if knobs.get("PDM_HIPCC_FLAGS"):                  # compiler experiments (diagnostic builds)
         flags += os.environ["PDM_HIPCC_FLAGS"].split()
     return flags
 
@@ -92,7 +93,7 @@ def file_flags():
     """FILE_FLAGS, overridden per file by $PDM_FILE_FLAGS ("rel/path.hip=flags;..."; diagnostic
     builds)."""
     ff = dict(FILE_FLAGS)
-    for item in filter(None, os.environ.get("PDM_FILE_FLAGS", "").split(";")):
+    for item in filter(None, knobs.get("PDM_FILE_FLAGS", "").split(";")):
         path, _, fl = item.partition("=")
         ff[path.strip()] = fl.split()
     return ff

@@ -1,0 +1,90 @@
+"""Every ``PDM_*`` environment knob in one registry.
+
+The defaults are the production configuration; a knob exists to force one of the structures
+``bench.py`` otherwise calibrates, to run a rehearsal on one GPU, or for a diagnostic or
+tuning experiment.  Code reads knobs through :func:`get` (an unregistered name is a bug and
+raises), ``bench.py`` echoes every knob that is set in its JSON line, and :func:`unknown`
+lists ``PDM_*`` variables that match no knob (a mistyped name would otherwise be ignored
+silently).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+# name -> (default, kind, meaning).  kind: "structure" = picks a step structure the default
+# chooses by itself, "rehearsal" = multi-rank tests on one GPU, "diag" = diagnostics and
+# experiments (timed runs leave them unset), "build" = extension build options.
+KNOBS: Dict[str, tuple] = {
+    # step structure (bf16 CNN)
+    "PDM_RCCL_MODE": ("carry", "structure",
+                      "RCCL step structure of the fc bucket: carry / nocarry / side / early / "
+                      "zero (bench.py calibrates all of them when unset)"),
+    "PDM_SHARD_FC": ("0", "structure", "1: shard the fc1 update over the ranks in bench.py"),
+    "PDM_COMM": ("auto", "structure", "gradient transport: auto / xgmi / rccl"),
+    "PDM_FUSE_CONV_REDUCE": ("1", "structure", "0: separate conv_reduce at world size 1"),
+    "PDM_FUSE_FC1": ("1", "structure", "0: fc1's SGD update in the optimizer launch, not fc1_bwd"),
+    "PDM_FC1_WT2": ("1", "structure", "0: the optimizer re-derives W1^T (no double buffer)"),
+    "PDM_KEEP_GRADS": ("0", "diag", "1: store the fc1 weight gradient the fused update consumes"),
+    "PDM_SPLITK_CAP": ("32", "structure", "largest fc1_fwd split-K factor"),
+    "PDM_BANDS": (None, "structure", "row bands per image in the conv backward (1 = off)"),
+    "PDM_FWD_BANDS": (None, "structure", "row bands of the forward alone"),
+    "PDM_GRAPH_STEPS": ("8", "structure", "training steps per captured hipGraph (power of two)"),
+    "PDM_AHEAD_GATHER_WGS": ("0", "structure", "workgroups of the ahead-of-time epoch gather"),
+    "PDM_FUSE_LIN_REDUCE": ("1", "structure", "0: separate lin_reduce at world size 1 (Linear)"),
+    "PDM_LIN_ROWS": (None, "diag", "rows per lin_train workgroup (kernel build constant)"),
+    "PDM_F32_CONV": ("x3", "structure", "fp32 CNN conv2 products: x3 (split-bf16) / exact"),
+    "PDM_F32_IPB": (None, "structure", "images per fp32 conv-backward workgroup"),
+    # xGMI transport
+    "PDM_XGMI_MODE": ("auto", "structure", "xgmi schedule: auto / one / two"),
+    "PDM_XGMI_STREAM": ("1", "structure", "0: per-bucket xgmi launches, no persistent kernel"),
+    "PDM_XGMI_EARLY": ("1", "structure", "0: xgmi fc bucket after the conv backward"),
+    "PDM_XGMI_OPT_WAIT": ("0", "structure", "1: optimizer workgroups wait per bucket"),
+    "PDM_XGMI_TIMEOUT": ("60", "structure", "seconds any xgmi wait for a peer may take"),
+    # bench.py
+    "PDM_FORCE_COMM": ("0", "diag", "1: the world-size>1 chain at N=1 (1-rank communicator)"),
+    "PDM_BENCH_BACKEND": ("nccl", "rehearsal", "gloo: multi-rank bench on one GPU"),
+    "PDM_BENCH_BOUNDARY": ("1", "diag", "0: no epoch boundary inside the timed window"),
+    "PDM_BENCH_DEBUG": (None, "diag", "1: print the host timeline of the timed window"),
+    "PDM_BENCH_FAIL_RANK": (None, "diag", "fault injection: this rank exits (dry runs)"),
+    "PDM_BENCH_SPAWNED": (None, "internal", "set by bench.py on the ranks it starts"),
+    "PDM_GATHER_AHEAD": ("1", "diag", "0: gather each epoch at its boundary"),
+    # rehearsal / runtime
+    "PDM_SHARE_DEVICE": ("0", "rehearsal", "1: every rank on device 0 (gloo / xgmi tests)"),
+    "PDM_ROCTX": ("1", "diag", "0: no roctx ranges even with --trace"),
+    "PDM_EXT_PATH": (None, "diag", "load this extension build instead of the in-tree one"),
+    # extension build
+    "PDM_DEBUG_BOUNDS": (None, "build", "device-side bounds checks"),
+    "PDM_STAMPS": (None, "build", "s_memtime phase stamps (diagnostic build)"),
+    "PDM_DIAG_ROLES": (None, "build", "fc1_bwd single-role launches"),
+    "PDM_NT": (None, "build", "non-temporal slab stores / loads"),
+    "PDM_ABL": (None, "build", "timing ablations"),
+    "PDM_DG_MTP": (None, "build", "cnn_bwd dgrad tiles per pass"),
+    "PDM_DG_PFD": (None, "build", "cnn_bwd dgrad prefetch distance"),
+    "PDM_HIPCC_FLAGS": (None, "build", "extra hipcc flags"),
+    "PDM_FILE_FLAGS": (None, "build", "per-file hipcc flags"),
+}
+
+
+def get(name: str, default: Optional[str] = None) -> Optional[str]:
+    """os.environ.get for a registered knob (the registry's default is documentation: the
+    call site's default is what applies, so an unset knob can be told apart)."""
+    if name not in KNOBS:
+        raise KeyError(f"unregistered knob {name} (add it to pytorch_distributed_mnist_amd/knobs.py)")
+    return os.environ.get(name, default)
+
+
+def is_set(name: str) -> bool:
+    if name not in KNOBS:
+        raise KeyError(f"unregistered knob {name}")
+    return name in os.environ
+
+
+def active() -> Dict[str, str]:
+    """Every PDM_* variable set in the environment (registered or not)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("PDM_")}
+
+
+def unknown() -> Dict[str, str]:
+    """PDM_* variables that match no knob (likely typos)."""
+    return {k: v for k, v in active().items() if k not in KNOBS}

@@ -16,6 +16,7 @@ import os
 import sys
 
 import torch  # noqa: F401  (binds the HIP runtime / RCCL before our .so loads)
+from .. import knobs
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _MOD = None
@@ -23,7 +24,7 @@ _ERR = None
 
 
 def ext_path():
-    override = os.environ.get("PDM_EXT_PATH")   # diagnostic builds (e.g. PDM_STAMPS)
+    override = knobs.get("PDM_EXT_PATH")   # diagnostic builds (e.g. PDM_STAMPS)
     if override:
         return override
     cands = sorted(glob.glob(os.path.join(_PKG_DIR, "_C*.so")))

@@ -24,6 +24,7 @@ from typing import Optional
 
 import torch
 import torch.distributed as dist
+from .. import knobs
 
 
 def distributed_is_initialized() -> bool:
@@ -51,7 +52,7 @@ def pick_device(local_rank: int, want: str = "auto") -> torch.device:
         return torch.device("cpu")
     if want in ("auto", "cuda") and torch.cuda.is_available():
         n = torch.cuda.device_count()
-        if os.environ.get("PDM_SHARE_DEVICE") == "1":
+        if knobs.get("PDM_SHARE_DEVICE") == "1":
             # test rehearsal only: every rank on device 0 (gloo data plane; RCCL refuses
             # two ranks on one GPU) to exercise the multi-rank GPU program on a 1-GPU box
             torch.cuda.set_device(0)

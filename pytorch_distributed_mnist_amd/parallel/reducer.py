@@ -38,12 +38,13 @@ import torch
 
 from ..ops import _ext
 from .comm import Communicator, RcclComm, TorchComm
+from .. import knobs
 
 TRANSPORTS = ("auto", "xgmi", "rccl")
 
 
 def default_transport() -> str:
-    t = os.environ.get("PDM_COMM", "auto")
+    t = knobs.get("PDM_COMM", "auto")
     if t not in TRANSPORTS:
         raise ValueError(f"PDM_COMM={t!r}: choose from {TRANSPORTS}")
     return t
@@ -83,7 +84,7 @@ class GradReducer:
                 self._xgmi = x
                 # streamed mode (default): one persistent collective launch per captured
                 # step sequence, hand-offs through device words (csrc/xgmi.h)
-                self.streamed = os.environ.get("PDM_XGMI_STREAM", "1") != "0"
+                self.streamed = knobs.get("PDM_XGMI_STREAM", "1") != "0"
                 self.sync = x.native.sync()
                 self.timeout_s = x.timeout_s
                 return
@@ -247,9 +248,9 @@ class XgmiTransport:
         from .dist import control_barrier, default_store, distributed_is_initialized
         ws, rank = comm.world_size, comm.rank
         dev = grads.device.index or 0
-        mode = mode or os.environ.get("PDM_XGMI_MODE", "auto")
+        mode = mode or knobs.get("PDM_XGMI_MODE", "auto")
         # bound on any wait for a peer inside the kernel (a late peer is an error, not a hang)
-        timeout_s = timeout_s or float(os.environ.get("PDM_XGMI_TIMEOUT", "60"))
+        timeout_s = timeout_s or float(knobs.get("PDM_XGMI_TIMEOUT", "60"))
         flat = [b for se in bounds for b in se]
         err = None
         native = None

@@ -22,6 +22,7 @@ import os
 import torch
 
 from .gpu_step import GpuStepBase
+from .. import knobs
 
 EVAL_CHUNK = 2048
 SPLITK_TRAIN = 32        # fc1 split-K (divides 288: whole 32-float k chunks per split)
@@ -30,7 +31,7 @@ SPLITK_TRAIN = 32        # fc1 split-K (divides 288: whole 32-float k chunks per
 def conv_ipb(B: int) -> int:
     """Images per fp32 conv-backward workgroup (each workgroup stages W2^T once and writes one
     slab for its images' row band): PDM_F32_IPB overrides."""
-    env = os.environ.get("PDM_F32_IPB")
+    env = knobs.get("PDM_F32_IPB")
     if env:
         return max(1, int(env))
     # B = 256, 100-step bench: ipb 1 / 2 / 3 / 6 = 360 / 351 / 340 / 416 us per step
@@ -81,7 +82,7 @@ class CnnStepF32(GpuStepBase):
         # cuDNN's default for fp32 convolutions -- 2.9e-4 (tests/test_split_bf16.py); the
         # step's gradients stay within 1e-4 of fp64 (tests/test_gpu_cnn_f32.py).
         # "exact" = the fp32 MFMA (exact fp32 products, 1.9x the step time).
-        mode = os.environ.get("PDM_F32_CONV", "x3")
+        mode = knobs.get("PDM_F32_CONV", "x3")
         if mode not in ("x3", "exact"):
             raise ValueError(f"PDM_F32_CONV={mode!r}: x3 or exact")
         self.conv_x3 = mode == "x3"

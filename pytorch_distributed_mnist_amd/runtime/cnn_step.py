@@ -28,6 +28,7 @@ import os
 import torch
 
 from .gpu_step import GpuStepBase
+from .. import knobs
 
 EVAL_CHUNK = 2048
 
@@ -82,7 +83,7 @@ def choose_bands(B: int, cus: int = 256) -> int:
     split of the node batch, 256 / world_size) spread each image over up to 6 workgroups
     (cnn_bwd_band.hip) so that B * bands fills at most one round of the CUs; 1 = cnn_bwd
     (PDM_BANDS overrides: 1 disables the split)."""
-    forced = os.environ.get("PDM_BANDS")
+    forced = knobs.get("PDM_BANDS")
     if forced is not None:
         return int(forced)
     for s in BAND_CHOICES:
@@ -95,7 +96,7 @@ def choose_fwd_bands(B: int) -> int:
     """Row bands per image in the forward: the backward's split (the band backward reads the
     band forward's a1 / normalised x); PDM_FWD_BANDS forces a split of the forward alone (it
     then hands the one-image backward the uint8 image, as cnn_fwd does)."""
-    forced = os.environ.get("PDM_FWD_BANDS")
+    forced = knobs.get("PDM_FWD_BANDS")
     if forced is not None and choose_bands(B) == 1:
         return int(forced)
     return choose_bands(B)
@@ -120,7 +121,7 @@ class CnnStep(GpuStepBase):
         self.pmask = torch.empty(cap * 9216, dtype=torch.uint8, device=dev)
         self.xg = torch.empty(B * 784, dtype=torch.uint8, device=dev)
         self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
-        self.splitk_train = choose_splitk(B, cap=int(os.environ.get("PDM_SPLITK_CAP", "32")))
+        self.splitk_train = choose_splitk(B, cap=int(knobs.get("PDM_SPLITK_CAP", "32")))
         self.splitk_eval = choose_splitk(min(cap, EVAL_CHUNK))
         part_n = max(self.splitk_train * B, self.splitk_eval * EVAL_CHUNK) * 128
         self.part = torch.empty(part_n, dtype=torch.float32, device=dev)
@@ -159,21 +160,21 @@ class CnnStep(GpuStepBase):
         # world_size 1 (no all-reduce between backward and update): the conv gradient
         # reduction is fused into the optimizer launch (PDM_FUSE_CONV_REDUCE=0 disables)
         self.fuse_conv_reduce = (not self.reducer.active and
-                                 os.environ.get("PDM_FUSE_CONV_REDUCE", "1") != "0")
+                                 knobs.get("PDM_FUSE_CONV_REDUCE", "1") != "0")
         # world_size 1, SGD-momentum: the fc1-weight update runs in fc1_bwd's weight-gradient
         # tiles (the gradient is still in registers; those tiles have slack next to the dX
         # tiles of the same launch); the optimizer launch then only re-derives the transposed
         # bf16 copy W1^T from the updated W1 (PDM_FUSE_FC1=0 disables)
         self.fuse_fc1 = (self.fuse_conv_reduce and self.opt.kind == "sgd" and
-                         os.environ.get("PDM_FUSE_FC1", "1") != "0")
+                         knobs.get("PDM_FUSE_FC1", "1") != "0")
         # ... and writes W1^T too, double-buffered by step parity (this step's dX tiles read
         # one half while its weight tiles write the other), so the optimizer launch skips fc1
         # entirely (PDM_FC1_WT2=0: the optimizer re-derives W1^T instead)
-        self.wt_double = os.environ.get("PDM_FC1_WT2", "1") != "0"
+        self.wt_double = knobs.get("PDM_FC1_WT2", "1") != "0"
         # the fused fc1 update consumes the fc1-weight gradient in registers; it is stored to
         # the gradient arena only when something will read it (tests comparing gradients set
         # keep_grads; PDM_KEEP_GRADS=1 forces it): 4.7 MB of writes per step otherwise
-        self.keep_grads = os.environ.get("PDM_KEEP_GRADS", "0") == "1"
+        self.keep_grads = knobs.get("PDM_KEEP_GRADS", "0") == "1"
         self.phase_period = 2 if self._wt_double_on() else 1
         self._fused = {}
         # RCCL data plane: where the fc bucket's all-reduce and update go (RCCL_MODES;
@@ -188,7 +189,7 @@ class CnnStep(GpuStepBase):
         #          DDP's Reducer does during loss.backward() (multi_proc_single_gpu.py:91); at
         #          small batches cnn_bwd_band leaves CUs free for RCCL's kernel (B = 32: 192
         #          workgroups on 256 CUs), at B = 256 the collective waits for cnn_bwd
-        self.set_rccl_mode(os.environ.get("PDM_RCCL_MODE", "carry"), invalidate=False)
+        self.set_rccl_mode(knobs.get("PDM_RCCL_MODE", "carry"), invalidate=False)
         # world_size > 1: optimizer-state sharding of the fc1 weight (set_shard_fc): its
         # gradient is reduce-scattered instead of all-reduced, each rank updates its
         # 128 / world_size rows (fp32 master, momentum, bf16 W1 rows) and the bf16 W1 rows are
@@ -404,7 +405,7 @@ class CnnStep(GpuStepBase):
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
         rccl_early = (self.fc_early and not xgmi and red.active and
                       getattr(red, "_native", None) is not None)
-        early = xgmi and not red.streamed and os.environ.get("PDM_XGMI_EARLY", "1") != "0"
+        early = xgmi and not red.streamed and knobs.get("PDM_XGMI_EARLY", "1") != "0"
         if rccl_early:
             # bucket 0 (fc, 4.7 MB) is complete: its all-reduce goes out now, on the
             # high-priority comm stream, beside the conv backward

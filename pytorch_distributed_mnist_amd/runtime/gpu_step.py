@@ -22,9 +22,10 @@ import os
 import torch
 
 from ..ops import _ext
+from .. import knobs
 
 
-_GRAPH_STEPS = int(os.environ.get("PDM_GRAPH_STEPS", "8"))   # steps per graph: a power of two
+_GRAPH_STEPS = int(knobs.get("PDM_GRAPH_STEPS", "8"))   # steps per graph: a power of two
 if _GRAPH_STEPS <= 0 or _GRAPH_STEPS & (_GRAPH_STEPS - 1):
     # train_steps splits a remainder into the set bits of GRAPH_SIZES: other sizes would
     # replay the wrong number of steps and desynchronise the device and host counters
@@ -90,7 +91,7 @@ class GpuStepBase:
     # -- data ----------------------------------------------------------------
     # workgroups of the ahead-of-time gather that runs beside the steps (0: one per 16 rows);
     # grid-striding workgroups take fewer CUs for longer
-    AHEAD_GATHER_WGS = int(os.environ.get("PDM_AHEAD_GATHER_WGS", "0"))
+    AHEAD_GATHER_WGS = int(knobs.get("PDM_AHEAD_GATHER_WGS", "0"))
 
     def _stage(self, idx: torch.Tensor) -> list:
         """Copy an epoch order into the next pinned staging buffer of a ring of three ([buffer,
@@ -321,7 +322,7 @@ class GpuStepBase:
         xg = {}
         if red.streamed:
             waits = red.waits_for(segs)
-            if os.environ.get("PDM_XGMI_OPT_WAIT") == "1":
+            if knobs.get("PDM_XGMI_OPT_WAIT") == "1":
                 xg = dict(xg=red.sync, signal_ch=signal_ch, waits=waits, timeout_s=red.timeout_s)
             else:
                 uniq = []
@@ -368,7 +369,7 @@ class LinearStep(GpuStepBase):
         # world size 1 (no all-reduce between backward and update): the slab reduction runs
         # inside the optimizer launch (PDM_FUSE_LIN_REDUCE=0 disables)
         self.fuse_reduce = (not self.reducer.active and
-                            os.environ.get("PDM_FUSE_LIN_REDUCE", "1") != "0")
+                            knobs.get("PDM_FUSE_LIN_REDUCE", "1") != "0")
         self._fused = {}
 
     def invalidate_graphs(self) -> None:

@@ -14,6 +14,7 @@ import contextlib
 import ctypes
 import ctypes.util
 import os
+from .. import knobs
 
 _lib = None
 _enabled = False
@@ -66,5 +67,5 @@ def mark(name: str) -> None:
         _lib.roctxMarkA(name.encode())
 
 
-if os.environ.get("PDM_ROCTX", "") not in ("", "0"):
+if knobs.get("PDM_ROCTX", "") not in ("", "0"):
     enable(True)
