@@ -1,30 +1,39 @@
 # Round-end refresh of the measured state: full GPU test suite, N=1 benches (driver length,
-# default, two epoch boundaries, fp32, the N>1 chain priced through a 1-rank RCCL communicator,
-# Linear, the strong-scaling per-rank batches), kbench, in-step kernel traces summarised on the
-# box, PMC passes.  Everything lands in gpurun_out/refresh/ (small text files).
+# default, two epoch boundaries, fp32 split-bf16 / exact, the N>1 chain priced through a 1-rank
+# RCCL communicator, Linear, the strong-scaling per-rank batches, the self-spawned two-rank
+# rehearsal), kbench, in-step kernel traces summarised on the box, PMC tables.  Everything
+# lands in gpurun_out/refresh/ (small text files).
 set -o pipefail
 O=gpurun_out/refresh
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
 : > $O/bench.jsonl
-run() { timeout -k 10 240 "$@" >> $O/bench.jsonl 2>> $O/bench.err || exit 1; }
+run() { timeout -k 10 300 "$@" >> $O/bench.jsonl 2>> $O/bench.err || exit 1; }
 run python bench.py --gpus 1 --steps 20 --warmup 5
 run python bench.py --gpus 1 --steps 20 --warmup 5
 run python bench.py
 run python bench.py --steps 470
 run python bench.py --dtype fp32
+PDM_F32_CONV=exact run python bench.py --dtype fp32
 PDM_FORCE_COMM=1 run python bench.py
 run python bench.py --model linear
 for B in 32 64 128; do
   run python bench.py --scaling weak --batch-per-rank $B
   PDM_FORCE_COMM=1 run python bench.py --scaling weak --batch-per-rank $B
 done
+PDM_SHARE_DEVICE=1 PDM_BENCH_BACKEND=gloo run python bench.py --gpus 2 --steps 20 --warmup 5
 timeout -k 10 300 python -u tools/kbench.py 32 64 128 256 1024 > $O/kbench.log 2>&1 || exit 1
 for B in 256 32; do
   d=$O/trace_$B
   timeout -k 10 180 rocprofv3 --kernel-trace -d $d -o run -- python3 bench.py --scaling weak --batch-per-rank $B --steps 200 --warmup 30 > /dev/null 2>&1 || exit 1
-  python tools/rocpd_summary.py $(ls $d/*.db | head -1) --title "in-step kernels, bench.py B=$B, 200 steps" --steps 150 > $O/trace_$B.md && rm -rf $d
+  python tools/rocpd_summary.py $(ls $d/*.db) --title "in-step kernels, bench.py B=$B, 200 steps" --steps 150 > $O/trace_$B.md && rm -rf $d
 done
-bash tools/pmc_run.sh > $O/pmc_run.log 2>&1 && cp gpurun_out/pmc.md $O/pmc.md && rm -rf gpurun_out/pmc
+d=$O/trace_f32
+timeout -k 10 180 rocprofv3 --kernel-trace -d $d -o run -- python3 bench.py --dtype fp32 --steps 200 --warmup 30 > /dev/null 2>&1 || exit 1
+python tools/rocpd_summary.py $(ls $d/*.db) --title "in-step kernels, bench.py --dtype fp32 (split-bf16 conv2) B=256, 200 steps" --steps 150 > $O/trace_f32.md && rm -rf $d
+bash tools/pmc_run.sh b256 256 bf16 > $O/pmc_b256.log 2>&1 || exit 1
+bash tools/pmc_run.sh b32force 32 bf16 force > $O/pmc_b32.log 2>&1 || exit 1
+bash tools/pmc_run.sh f32 256 fp32 > $O/pmc_f32.log 2>&1 || exit 1
+cp gpurun_out/pmc/*.md $O/ && rm -rf gpurun_out/pmc
 echo rc=$?
