@@ -7,10 +7,13 @@ counter group, tools/pmc_run.sh) and the ``*kernel_trace.csv`` of a ``--kernel-t
 the same program (kernel durations).  Every value is the mean over the kernel's dispatches.
 
 Derived columns (units and sources; MI355X_MICROARCH.md, "rocprofv3 PMC slots", "DVFS"):
-  dur us        kernel-trace End - Start
-  clk GHz       GRBM_GUI_ACTIVE / 8 XCDs / dur (reads high on short dispatches)
+  dur us        kernel-trace End - Start (back-to-back dispatches: includes the launch gap)
   waves/CU      SQ_WAVES / 256 CUs
-  MFMA busy %   SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+  MFMA busy %   SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x dur x 2.4 GHz): the share of the
+                dispatch's SIMD-cycles the matrix cores were busy, at the peak clock (a lower
+                bound when the chip runs slower).  GRBM_GUI_ACTIVE / 8 / dur reads 3-6 GHz on
+                these microsecond dispatches (MI355X_MICROARCH.md: it reads high below
+                ~0.3 ms), so it is not used as the clock
   VALU/wave     SQ_INSTS_VALU / SQ_WAVES (wave64 vector instructions, MFMA included)
   LDS confl %   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles over LDS-active cycles)
   wait %        SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
@@ -68,7 +71,7 @@ def load_durations(files):
 
 
 def table(counters, durations, title=""):
-    hdr = ["kernel", "dur us", "clk GHz", "waves/CU", "MFMA busy %", "VALU/wave",
+    hdr = ["kernel", "dur us", "waves/CU", "MFMA busy %", "VALU/wave",
            "LDS confl %", "wait %", "issue-stall %", "rd MB", "wr MB", "GB/s", "L2 hit %"]
     rows = [f"### {title}" if title else "", "", "| " + " | ".join(hdr) + " |",
             "|---|" + "---:|" * (len(hdr) - 1)]
@@ -79,13 +82,12 @@ def table(counters, durations, title=""):
         d = counters[k]
         f = lambda c: d.get(c, nan)
         us = durations.get(k, (nan, 0))[0]
-        gui = f("GRBM_GUI_ACTIVE") / 8
         waves = f("SQ_WAVES")
         rd = f("FETCH_SIZE") * 1024 / 1e6
         wr = f("WRITE_SIZE") * 1024 / 1e6
         hit, miss = f("TCC_HIT_sum"), f("TCC_MISS_sum")
-        cells = [k, f"{us:.2f}", f"{gui / (us * 1e3):.2f}", f"{waves / 256:.1f}",
-                 f"{100 * f('SQ_VALU_MFMA_BUSY_CYCLES') / (1024 * gui):.1f}",
+        cells = [k, f"{us:.2f}", f"{waves / 256:.1f}",
+                 f"{100 * f('SQ_VALU_MFMA_BUSY_CYCLES') / (1024 * us * 2.4e3):.1f}",
                  f"{f('SQ_INSTS_VALU') / waves:.0f}",
                  f"{100 * f('SQ_LDS_BANK_CONFLICT') / f('SQ_LDS_IDX_ACTIVE'):.1f}"
                  if f("SQ_LDS_IDX_ACTIVE") > 0 else "-",
