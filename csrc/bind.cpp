@@ -697,16 +697,19 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
                  ylab.data_ptr<int32_t>(), x3, cur_stream(images));
 }
 
-void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int64_t splitk) {
+void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int64_t splitk,
+                 bool x3) {
   c10::DeviceGuard g(pool.device());
   TORCH_CHECK(B >= 1 && splitk >= 1 && 288 % splitk == 0, "splitk must divide 288");
+  // the split-bf16 kernel stages whole 96-feature batches
+  TORCH_CHECK(!x3 || 96 % splitk == 0, "split-bf16 fc1: splitk must divide 96");
   need_min(pool, at::kFloat, B * CNN_FEAT, "pool");
   need(w1, at::kFloat, "w1");
   TORCH_CHECK(w1.numel() == (int64_t)CNN_HID * CNN_FEAT, "fc1 weight");
   need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
   for (const void* q : {pool.data_ptr(), w1.data_ptr()}) need_aligned(q, 16, "fc1 operand");
   launch_f32_fc1_fwd(pool.data_ptr<float>(), w1.data_ptr<float>(), part.data_ptr<float>(), (int)B,
-                     (int)splitk, cur_stream(pool));
+                     (int)splitk, x3, cur_stream(pool));
 }
 
 void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int64_t B,
@@ -831,7 +834,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"), py::arg("pool"),
         py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"), py::arg("spe") = 0,
         py::arg("x3") = false);
-  m.def("f32_fc1_fwd", &f32_fc1_fwd);
+  m.def("f32_fc1_fwd", &f32_fc1_fwd, py::arg("pool"), py::arg("w1"), py::arg("part"), py::arg("B"),
+        py::arg("splitk"), py::arg("x3") = false);
   m.def("f32_fc1_bwd", &f32_fc1_bwd);
   m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1,

@@ -227,7 +227,7 @@ void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, 
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
                     int32_t* ylab, bool x3, hipStream_t st);
 void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,
-                        hipStream_t st);
+                        bool x3, hipStream_t st);
 void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
                         float* gwf1, float* dpool, const float* head_slab, int head_blocks,
                         float* gwf2, float* gbf2, float* gbf1, double* metrics, hipStream_t st);

@@ -398,6 +398,112 @@ __global__ __launch_bounds__(256) void f32_fc1_fwd_kernel(const float* __restric
     }
 }
 
+// f32x3_fc1_fwd: f32_fc1_fwd on split-bf16 products.  Per batch of XK k-steps (96 features)
+// the pool rows and W1 rows are split into hi / lo bf16 planes in LDS (row pitch 208 B:
+// the 16 rows of a fragment read land on distinct bank quads), then 3 MFMAs per 16x16x32
+// block.  XCD-aware grid as the bf16 fc1_fwd: with S % 8 == 0 every XCD owns S / 8 splits for
+// all m-tiles, so its L2 serves W1's slice to each m-tile after the first (the fp32 kernel
+// re-read all of W1 per m-tile from HBM: 24 MB per step at B = 256, L2 hit 9 %).
+constexpr int XK = 3;
+constexpr int XKP = XK * 32 * 2 + 16;             // 208 B
+constexpr int XF_BH = 2 * 32 * XKP, XF_BL = XF_BH + HID * XKP;
+constexpr int XF1_TOTAL = XF_BL + HID * XKP;       // 66560 B: 2 workgroups / CU
+
+__device__ __forceinline__ void split4_store(char* hi, char* lo, float4 v) {
+  const float f[4] = {v.x, v.y, v.z, v.w};
+  bf16x4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = to_bf16(f[j]);
+    l[j] = to_bf16(f[j] - from_bf16(h[j]));
+  }
+  *reinterpret_cast<bf16x4*>(hi) = h;
+  *reinterpret_cast<bf16x4*>(lo) = l;
+}
+
+__global__ __launch_bounds__(256, 2) void f32x3_fc1_fwd_kernel(const float* __restrict__ pool,
+                                                               const float* __restrict__ w1,
+                                                               float* __restrict__ part, int B,
+                                                               int kchunk) {
+  __shared__ __attribute__((aligned(16))) char sm[XF1_TOTAL];
+  const int mtiles = (B + 31) / 32, S = FEAT / kchunk;
+  const int w = blockIdx.x;
+  int mtile, sidx;
+  if (S % 8 == 0) {
+    const int xcd = w % 8, loc = w / 8, spx = S / 8;
+    sidx = xcd * spx + loc % spx;
+    mtile = loc / spx;
+  } else {
+    sidx = w / mtiles;
+    mtile = w % mtiles;
+  }
+  const int b0 = mtile * 32, kbeg = sidx * kchunk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int C4 = XK * 8;                        // float4 per staged row (24)
+  for (int kb = 0; kb < kchunk; kb += 32 * XK) {
+    float4 av[3], wv[12];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {                   // A: 32 rows x 24 float4 (rows past B clamped)
+      const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
+      av[u] = *reinterpret_cast<const float4*>(pool + (int64_t)min(b0 + r, B - 1) * FEAT + kbeg + kb + 4 * c4);
+    }
+#pragma unroll
+    for (int u = 0; u < 12; ++u) {                  // B: 128 rows x 24 float4
+      const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
+      wv[u] = *reinterpret_cast<const float4*>(w1 + (int64_t)r * FEAT + kbeg + kb + 4 * c4);
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
+      split4_store(sm + r * XKP + 8 * c4, sm + (32 + r) * XKP + 8 * c4, av[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 12; ++u) {
+      const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
+      split4_store(sm + XF_BH + r * XKP + 8 * c4, sm + XF_BL + r * XKP + 8 * c4, wv[u]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < XK; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int o = (mt * 16 + i16) * XKP + ks * 64 + g * 16;
+        ah[mt] = *reinterpret_cast<const bf16x8*>(sm + o);
+        al[mt] = *reinterpret_cast<const bf16x8*>(sm + 32 * XKP + o);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int o = (wave * 32 + nt * 16 + i16) * XKP + ks * 64 + g * 16;
+        bh[nt] = *reinterpret_cast<const bf16x8*>(sm + XF_BH + o);
+        bl[nt] = *reinterpret_cast<const bf16x8*>(sm + XF_BL + o);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma3(ah[mt], al[mt], bh[nt], bl[nt], acc[mt][nt]);
+    }
+    __syncthreads();   // this batch's reads are done before the next batch's staging
+  }
+  float* out = part + (int64_t)sidx * B * HID;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rowi = b0 + mt * 16 + 4 * g + r;
+      if (rowi < B) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) out[(int64_t)rowi * HID + wave * 32 + nt * 16 + i16] = acc[mt][nt][r];
+      }
+    }
+}
+
 // ------------------------------------------------------------------ f32_fc1_bwd
 constexpr int DWF = 64;                 // dW tile: 128 n x 64 features
 constexpr int DW_T = FEAT / DWF;        // 144
@@ -803,9 +909,28 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     *reinterpret_cast<bf16x8*>(smem + XB_WH + xw_off(tap, ci, c)) = h;
     *reinterpret_cast<bf16x8*>(smem + XB_WL + xw_off(tap, ci, c)) = l;
   }
-  // wgrad: this wave's co tile and (tap, ci tile) columns; per-lane tr-read pieces
+  // wgrad: this wave's co tile and (tap, ci tile) columns; per-lane tr-read pieces, image
+  // independent, so computed once: k-step ks covers run v = 4 ks + g = 8 pixels of output
+  // row v / 3 from column 8 (v % 3); the lane addresses pixels col0 + q (+ 4), columns
+  // 4 pq .. 4 pq + 3.  a1 pixel (r + ky, col0 + q + kx (+ 4)): col0 % 8 == 0, so the a1_off
+  // swizzle term depends on (q + kx) & 3 only -> a base per k-step + a constant per tap
   const int wmt = wave & 3, wn0 = 9 * (wave >> 2);
   const int q = (lane >> 2) & 3, pq = lane & 3;
+  int dza[3][2], a1b[3], a1s[3][2];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int v = 4 * ks + g, r = v / 3, col0 = (v - 3 * r) * 8;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int zp = 2 + (r + 2) * H1 + col0 + q + 4 * s2;
+      dza[ks][s2] = xdz_off(zp, 2 * wmt + (pq >> 1)) + 8 * (pq & 1);
+    }
+    a1b[ks] = (r * H1 + col0 + q) * 64 + 8 * (pq & 1);
+  }
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) a1s[kx][ct] = ((2 * ct + (pq >> 1)) ^ ((q + kx) & 3)) << 4;
   f32x4 wacc[9];
 #pragma unroll
   for (int j = 0; j < 9; ++j) wacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -851,30 +976,31 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
       }
     }
     __syncthreads();
-    // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad:
-    // units (pixel tile mt, ci tile nt), unit u = 2 mt + nt on wave u % 8 (7 or 10 tiles x 2
-    // = 14 or 20 units: at most 3 per wave, where whole tiles left two waves with twice the
-    // work of the others)
-    for (int u = wave; u < 2 * nmt; u += 8) {
-      const int mt = u >> 1, nt = u & 1;
+    // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
+    for (int mt = wave; mt < nmt; mt += 8) {
       const int p = min(mt * 16 + i16, npx - 1);
       const int y = p / H1, x = p - y * H1;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll 1
       for (int tap = 0; tap < 9; ++tap) {
         const int ky = tap / 3, kx = tap - 3 * ky;
         const int zp = 2 + (y + 2 - ky) * H1 + x - kx;
-        bf16x8 ah[2], al[2], bh[2], bl[2];
+        bf16x8 ah[2], al[2], bh[2][2], bl[2][2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           ah[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DH + xdz_off(zp, 4 * kk + g));
           al[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DL + xdz_off(zp, 4 * kk + g));
-          const int wo = xw_off(tap, nt * 16 + i16, 4 * kk + g);
-          bh[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_WH + wo);
-          bl[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_WL + wo);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const int wo = xw_off(tap, nt * 16 + i16, 4 * kk + g);
+            bh[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WH + wo);
+            bl[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WL + wo);
+          }
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) acc = mfma3(ah[kk], al[kk], bh[kk], bl[kk], acc);
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma3(ah[kk], al[kk], bh[kk][nt], bl[kk][nt], acc[nt]);
       }
       float xb[4];
       const int ctap = i16;
@@ -887,43 +1013,39 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
                 : ctap < 9 ? xs[(yy + ctap / 3) * IMG + xx + ctap % 3]
                 : ctap == 9 ? 1.f : 0.f;
         const int pc = min(pr, npx - 1);
-        // relu'(a1): a1 >= 0, so a1 > 0 iff its hi or lo part is non-zero
-        const int o = a1_off(pc / H1, pc % H1, 2 * (nt * 16 + i16));
-        const unsigned short hb = *reinterpret_cast<const unsigned short*>(smem + XB_AH + o);
-        const unsigned short lb = *reinterpret_cast<const unsigned short*>(smem + XB_AL + o);
-        acc[r] = (valid && (hb | lb) != 0) ? acc[r] : 0.f;
-      }
-      if (nt == 0) {                  // wave-uniform
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc1[0] = mfma4(acc[r], xb[r], acc1[0]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc1[1] = mfma4(acc[r], xb[r], acc1[1]);
+        for (int nt = 0; nt < 2; ++nt) {
+          // relu'(a1): a1 >= 0, so a1 > 0 iff its hi or lo part is non-zero
+          const int o = a1_off(pc / H1, pc % H1, 2 * (nt * 16 + i16));
+          const unsigned short hb = *reinterpret_cast<const unsigned short*>(smem + XB_AH + o);
+          const unsigned short lb = *reinterpret_cast<const unsigned short*>(smem + XB_AL + o);
+          acc[nt][r] = (valid && (hb | lb) != 0) ? acc[nt][r] : 0.f;
+        }
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
     }
     // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
     // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
     // the addresses of pixels col0 + q and col0 + 4 + q of that run, columns 4 pq .. 4 pq + 3
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) {
-      const int v = 4 * ks + g, r = v / 3, col0 = (v - 3 * r) * 8;
-      bf16x8 ah, al;
-      {
-        const int zp0 = 2 + (r + 2) * H1 + col0 + q, zp1 = zp0 + 4;
-        const int ch = 2 * wmt + (pq >> 1), bo = 8 * (pq & 1);
-        ah = cat_tr(lds_tr16(smem + XB_DH + xdz_off(zp0, ch) + bo),
-                    lds_tr16(smem + XB_DH + xdz_off(zp1, ch) + bo));
-        al = cat_tr(lds_tr16(smem + XB_DL + xdz_off(zp0, ch) + bo),
-                    lds_tr16(smem + XB_DL + xdz_off(zp1, ch) + bo));
-      }
+      const bf16x8 ah = cat_tr(lds_tr16(smem + XB_DH + dza[ks][0]), lds_tr16(smem + XB_DH + dza[ks][1]));
+      const bf16x8 al = cat_tr(lds_tr16(smem + XB_DL + dza[ks][0]), lds_tr16(smem + XB_DL + dza[ks][1]));
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
+        // (tap, ci tile) of column j: wave-uniform, so ky / kx / ct are per-wave values and
+        // the offset below is one add of a per-lane base and a small table entry
         const int nn = wn0 + j, tap = nn >> 1, ct = nn & 1;
         const int ky = tap / 3, kx = tap - 3 * ky;
-        const int o0 = a1_off(r + ky, col0 + q + kx, 2 * (ct * 16 + 4 * pq));
-        const int o1 = a1_off(r + ky, col0 + 4 + q + kx, 2 * (ct * 16 + 4 * pq));
-        const bf16x8 bh = cat_tr(lds_tr16(smem + XB_AH + o0), lds_tr16(smem + XB_AH + o1));
-        const bf16x8 bl = cat_tr(lds_tr16(smem + XB_AL + o0), lds_tr16(smem + XB_AL + o1));
+        const int s0 = ct ? a1s[0][1] : a1s[0][0], s1 = ct ? a1s[1][1] : a1s[1][0];
+        const int s2 = ct ? a1s[2][1] : a1s[2][0];
+        const int kxs = kx == 0 ? s0 : (kx == 1 ? s1 : s2);   // selects: no indexed registers
+        const int o0 = a1b[ks] + (ky * H1 + kx) * 64 + kxs;
+        const bf16x8 bh = cat_tr(lds_tr16(smem + XB_AH + o0), lds_tr16(smem + XB_AH + o0 + 256));
+        const bf16x8 bl = cat_tr(lds_tr16(smem + XB_AL + o0), lds_tr16(smem + XB_AL + o0 + 256));
         wacc[j] = mfma3(ah, al, bh, bl, wacc[j]);
       }
     }
@@ -980,7 +1102,11 @@ void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, 
 }
 
 void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,
-                        hipStream_t st) {
+                        bool x3, hipStream_t st) {
+  if (x3) {
+    f32x3_fc1_fwd_kernel<<<((B + 31) / 32) * splitk, 256, 0, st>>>(pool, w1, part, B, FEAT / splitk);
+    return;
+  }
   f32_fc1_fwd_kernel<<<((B + 31) / 32) * splitk, 256, 0, st>>>(pool, w1, part, B, FEAT / splitk);
 }
 

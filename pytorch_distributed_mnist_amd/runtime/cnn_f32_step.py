@@ -76,7 +76,7 @@ class CnnStepF32(GpuStepBase):
                                           "fc2.bias")}
         self.G = {n: a.grad(n) for n in self.P}
         self.fuse_conv_reduce = not self.reducer.active
-        # conv2 products (the step's FLOPs): "x3" (default) = split-bf16 on the bf16 MFMA
+        # conv2 and fc1-forward products (the step's FLOPs): "x3" (default) = split-bf16 on the bf16 MFMA
         # (hi.hi + hi.lo + lo.hi, fp32 accumulation; cnn_f32.hip f32x3_*): 4.5e-6 relative
         # error on a conv2 output against fp64, where exact fp32 gives 1.6e-7 and TF32 --
         # cuDNN's default for fp32 convolutions -- 2.9e-4 (tests/test_split_bf16.py); the
@@ -128,7 +128,7 @@ class CnnStepF32(GpuStepBase):
                   P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
                   self.pool, self.pmask, self.a1g, self.xng, self.ylab, spe=self.spe,
                   x3=self.conv_x3)
-        C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN)
+        C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN, x3=self.conv_x3)
         C.cnn_head(self.part, SPLITK_TRAIN, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                    self.ylab, True, None, None, ldt, self.head_slab, self.metrics.train_view(),
                    self.ctr[0:1], self.opt._step_dev, None, self.dh32)
@@ -159,6 +159,6 @@ class CnnStepF32(GpuStepBase):
             C.f32_fwd(self.test_images[s:s + b], self.test_labels[s:s + b], None, b, b,
                       P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
                       self.pool, None, None, None, self.ylab, x3=self.conv_x3)
-            C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, b, se)
+            C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, b, se, x3=self.conv_x3)
             C.cnn_head(self.part, se, b, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
                        False, None, None, 32, None, self.metrics.eval_view(), None, None)
