@@ -97,10 +97,16 @@ def test_two_ranks_on_one_gpu_match_one_rank(gpu, tmp_path, monkeypatch):
             assert err < tol, (ep, k, err)
 
 
-def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path):
-    """--arch cnn --dtype fp32 (the reference's precision, fp32 MFMA kernels): train, resume,
-    evaluate on the GPU, and the same run on the CPU path: every printed loss agrees to fp32
-    summation noise (the bf16 path agrees only to bf16 accuracy)."""
+@pytest.mark.parametrize("conv,loss_tol,acc_tol", [("exact", 5e-5, 0.1), ("x3", 2e-3, 0.5)])
+def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path, monkeypatch, conv, loss_tol,
+                                                        acc_tol):
+    """--arch cnn --dtype fp32: train, resume, evaluate on the GPU, and the same run on the CPU
+    path.  With exact fp32 products (PDM_F32_CONV=exact) every printed loss agrees to fp32
+    summation noise; with the default split-bf16 conv2 / fc1 products (4.5e-6 relative error
+    per conv2 output, tests/test_split_bf16.py) the losses agree to 2e-3 after two epochs of
+    SGD-momentum -- the trajectories drift apart as any two precisions' do (the bf16 path
+    agrees only to bf16 accuracy)."""
+    monkeypatch.setenv("PDM_F32_CONV", conv)
     d1, d2 = tmp_path / "gpu", tmp_path / "cpu"
     d1.mkdir()
     d2.mkdir()
@@ -112,9 +118,9 @@ def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path):
     for lg, lc in zip(g, c):
         mg, mc = EPOCH_RE.match(lg), EPOCH_RE.match(lc)
         for i in (3, 5):
-            assert abs(float(mg.group(i)) - float(mc.group(i))) < 5e-5, (lg, lc)
+            assert abs(float(mg.group(i)) - float(mc.group(i))) < loss_tol, (lg, lc)
         for i in (4, 6):
-            assert abs(float(mg.group(i)) - float(mc.group(i))) <= 0.1, (lg, lc)
+            assert abs(float(mg.group(i)) - float(mc.group(i))) <= acc_tol, (lg, lc)
     ck = d1 / "checkpoints" / "checkpoint_1.pth.tar"
     ev = [l for l in cli(["--arch", "cnn", "--optimizer", "sgd", "--dtype", "fp32", "--evaluate",
                           "--resume", str(ck)], d1) if l.startswith("test loss:")]
