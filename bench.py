@@ -60,7 +60,7 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--no-graphs", dest="graphs", action="store_false")
     ap.add_argument("--train-size", type=int, default=60000)
-    ap.add_argument("--timeout", type=float, default=600.0,
+    ap.add_argument("--timeout", type=float, default=180.0,
                     help="deadline (s) for RCCL init and every host sync")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous only (gloo, CPU): each rank joins the process "

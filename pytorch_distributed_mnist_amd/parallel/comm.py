@@ -152,12 +152,39 @@ def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | No
 
 
 def make_comm(ctx, force_native: bool = False) -> Communicator:
-    """Pick the data-plane communicator for a rank's DistContext."""
+    """Pick the data-plane communicator for a rank's DistContext.
+
+    ``--backend nccl`` on the GPU: the native C++ RCCL communicator.  Its bring-up is agreed
+    over the control plane: if any rank fails to create it (an RCCL error, or the init
+    deadline), every rank drops its own and the job continues on torch's ProcessGroupNCCL
+    (``TorchComm`` on the default group's cuda:nccl backend: the same RCCL collectives, not
+    capturable into the step graph, so steps run eagerly) with a warning, instead of one rank
+    raising while the others wait for it."""
     if ctx.world_size == 1 and not force_native and not ctx.initialized:
         return LocalComm()
     if ctx.is_gpu and ctx.backend == "nccl":
-        return RcclComm(ctx.rank, ctx.world_size, ctx.device,
-                        timeout_s=getattr(ctx, "timeout_s", 1800.0))
+        err, comm = None, None
+        try:
+            comm = RcclComm(ctx.rank, ctx.world_size, ctx.device,
+                            timeout_s=getattr(ctx, "timeout_s", 1800.0))
+        except Exception as e:                      # noqa: BLE001 (reported below)
+            err = e
+        ok = err is None
+        if ctx.world_size > 1 and distributed_is_initialized():
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)     # gloo: CPU tensor
+            ok = bool(t.item())
+        if ok:
+            return comm
+        if comm is not None:
+            comm.abort()
+        if not ctx.initialized:
+            raise RuntimeError(f"RCCL communicator bring-up failed: {err}")
+        import sys
+        print(f"warning: native RCCL communicator unavailable on rank {ctx.rank} "
+              f"({err or 'failed on another rank'}); using torch's ProcessGroupNCCL",
+              file=sys.stderr, flush=True)
+        return TorchComm()
     if ctx.initialized:
         return TorchComm()
     return LocalComm()
