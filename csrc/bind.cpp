@@ -657,10 +657,19 @@ void conv_reduce(at::Tensor slab, int64_t nblk, at::Tensor gw2, at::Tensor gb2, 
 int64_t cnn_bwd_nblk(int64_t B, int64_t ipb, int64_t bands) { return conv_blocks(B, ipb, bands); }
 
 // ------------------------------------------------------------------ CNN fp32 (cnn_f32.hip)
+// the split-bf16 W2^T planes the x3 forward writes for the x3 backward (2 x 36864 B)
+static float* w2x_ptr(const c10::optional<at::Tensor>& w2x) {
+  TORCH_CHECK(w2x.has_value() && w2x->defined(), "the split-bf16 path needs the w2x buffer");
+  need_min(*w2x, at::kFloat, 2 * 9 * 32 * 128 / 4, "w2x");
+  need_aligned(w2x->data_ptr(), 16, "w2x");
+  return w2x->data_ptr<float>();
+}
+
 void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr, int64_t bfull,
              int64_t B, at::Tensor w1, at::Tensor b1, at::Tensor w2, at::Tensor b2,
              at::Tensor pool, c10::optional<at::Tensor> pmask, c10::optional<at::Tensor> a1g,
-             c10::optional<at::Tensor> xng, at::Tensor ylab, int64_t spe, bool x3) {
+             c10::optional<at::Tensor> xng, at::Tensor ylab, int64_t spe, bool x3,
+             c10::optional<at::Tensor> w2x) {
   c10::DeviceGuard g(images.device());
   need(images, at::kByte, "images");
   need(labels, at::kInt, "labels");
@@ -694,7 +703,8 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
                  w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                  pool.data_ptr<float>(), train ? pmask->data_ptr<uint8_t>() : nullptr,
                  train ? a1g->data_ptr<float>() : nullptr, train ? xng->data_ptr<float>() : nullptr,
-                 ylab.data_ptr<int32_t>(), x3, cur_stream(images));
+                 ylab.data_ptr<int32_t>(), x3,
+                 train && x3 ? w2x_ptr(w2x) : nullptr, cur_stream(images));
 }
 
 void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int64_t splitk,
@@ -740,7 +750,7 @@ void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int
 }
 
 void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor pmask, at::Tensor w2,
-                  int64_t B, at::Tensor slab, int64_t ipb, bool x3) {
+                  int64_t B, at::Tensor slab, int64_t ipb, bool x3, c10::optional<at::Tensor> w2x) {
   c10::DeviceGuard g(a1g.device());
   TORCH_CHECK(B >= 1 && ipb >= 1, "B and ipb must be >= 1");
   need_min(a1g, at::kFloat, B * 676 * 32, "a1g");
@@ -753,7 +763,7 @@ void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor p
            "conv slab");
   launch_f32_conv_bwd(a1g.data_ptr<float>(), xng.data_ptr<float>(), dpool.data_ptr<float>(),
                       pmask.data_ptr<uint8_t>(), w2.data_ptr<float>(), (int)B, (int)ipb,
-                      slab.data_ptr<float>(), x3, cur_stream(a1g));
+                      slab.data_ptr<float>(), x3, x3 ? w2x_ptr(w2x) : nullptr, cur_stream(a1g));
 }
 
 // Upload an instantiated hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device
@@ -833,13 +843,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("f32_fwd", &f32_fwd, py::arg("images"), py::arg("labels"), py::arg("ctr"), py::arg("bfull"),
         py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"), py::arg("pool"),
         py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"), py::arg("spe") = 0,
-        py::arg("x3") = false);
+        py::arg("x3") = false, py::arg("w2x") = py::none());
   m.def("f32_fc1_fwd", &f32_fc1_fwd, py::arg("pool"), py::arg("w1"), py::arg("part"), py::arg("B"),
         py::arg("splitk"), py::arg("x3") = false);
   m.def("f32_fc1_bwd", &f32_fc1_bwd);
   m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1,
-        py::arg("x3") = false);
+        py::arg("x3") = false, py::arg("w2x") = py::none());
   m.def("f32_conv_bwd_nblk", [](int64_t B, int64_t ipb) {
     return (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb); }, py::arg("B"), py::arg("ipb") = 1);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);

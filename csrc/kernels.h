@@ -225,7 +225,7 @@ void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, flo
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
                     StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
-                    int32_t* ylab, bool x3, hipStream_t st);
+                    int32_t* ylab, bool x3, float* w2x, hipStream_t st);
 void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,
                         bool x3, hipStream_t st);
 void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
@@ -235,7 +235,7 @@ void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float
 int f32_conv_bwd_blocks(int B, int ipb);
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
                          const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
-                         bool x3, hipStream_t st);
+                         bool x3, const float* w2x, hipStream_t st);
 
 // diagnostic timestamps (all zero unless built with PDM_STAMPS=1)
 void read_stamps_fwd(unsigned long long* host);

@@ -196,6 +196,13 @@ __device__ __forceinline__ f32x4 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 b
 // its output a1 is stored as hi / lo bf16 planes in the bf16 forward's swizzled LDS layout
 // (cnn_common.h a1_off), and conv2 runs cnn_fwd's tiling (16-row tiles = 4 pooled pixels x
 // 2x2 window, one tap = one K = 32 step) with the W2 fragments split once into registers.
+// Training hands the backward its operands already split, in the backward's LDS layouts
+// (plain 16-B copies there instead of strided gathers + splitting per workgroup): the a1
+// planes of every image (a1x: [img][hi plane | lo plane], 2 x 43264 B, the fp32 a1g buffer's
+// size) and the W2^T planes (w2x: [hi | lo] x [tap][ci][64 co], chunk c at c ^ (ci & 7)),
+// the latter written by the first workgroups (grid-stride over its 2304 16-B chunks).
+constexpr int A1X_PLANE = P1 * 64;                 // bytes per a1 plane per image
+constexpr int W2X_PLANE = 9 * C1 * 128;            // bytes per W2^T plane
 constexpr int XF_XS = 0;                          // fp32 x [784]
 constexpr int XF_WS = 3136;                       // fp32 w1 [288] | b1 [32] | b2 [64]
 constexpr int XF_AH = 4736;                       // bf16 a1 hi plane [676 px][64 B], swizzled
@@ -208,8 +215,8 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels, int64_t nrow,
     const int64_t* __restrict__ ctr, const StepRows sr, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
-    float* __restrict__ pool, uint8_t* __restrict__ pmask, float* __restrict__ a1g,
-    float* __restrict__ xng, int32_t* __restrict__ ylab) {
+    float* __restrict__ pool, uint8_t* __restrict__ pmask, char* __restrict__ a1x,
+    float* __restrict__ xng, int32_t* __restrict__ ylab, char* __restrict__ w2x) {
   __shared__ __attribute__((aligned(16))) char smem[XF_TOTAL];
   float* xs = reinterpret_cast<float*>(smem + XF_XS);
   float* ws = reinterpret_cast<float*>(smem + XF_WS);
@@ -273,10 +280,24 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
       *reinterpret_cast<bf16x8*>(smem + XF_AH + off) = h;
       *reinterpret_cast<bf16x8*>(smem + XF_AL + off) = l;
       if (TRAIN) {
-        float4* dst = reinterpret_cast<float4*>(a1g + ((int64_t)img * P1 + p) * C1 + 8 * c8);
-        dst[0] = make_float4(o[0], o[1], o[2], o[3]);
-        dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+        char* dst = a1x + (int64_t)img * 2 * A1X_PLANE + off;
+        *reinterpret_cast<bf16x8*>(dst) = h;
+        *reinterpret_cast<bf16x8*>(dst + A1X_PLANE) = l;
       }
+    }
+  }
+  if (TRAIN) {
+    // W2^T planes for the backward: chunk (tap, c, ci) = co 8 c .. 8 c + 7 of (tap, ci)
+    for (int e = img * FT + tid; e < 9 * 8 * C1; e += gridDim.x * FT) {
+      const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = w2[(8 * c + u) * 288 + tap * 32 + ci];
+      bf16x8 h, l;
+      split8(v, h, l);
+      const int o = (tap * C1 + ci) * 128 + ((c ^ (ci & 7)) << 4);
+      *reinterpret_cast<bf16x8*>(w2x + o) = h;
+      *reinterpret_cast<bf16x8*>(w2x + W2X_PLANE + o) = l;
     }
   }
   __syncthreads();
@@ -883,8 +904,8 @@ __device__ __forceinline__ int xw_off(int tap, int ci, int chunk) {
 }
 
 __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
-    const float* __restrict__ a1g, const float* __restrict__ xng, const float* __restrict__ dpool,
-    const uint8_t* __restrict__ pmask, const float* __restrict__ w2, int B, int ipb,
+    const char* __restrict__ a1x, const float* __restrict__ xng, const float* __restrict__ dpool,
+    const uint8_t* __restrict__ pmask, const char* __restrict__ w2x, int B, int ipb,
     float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) char smem[XB_TOTAL];
   float* xs = reinterpret_cast<float*>(smem + XB_XS);
@@ -898,17 +919,9 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
   const int pr0 = band == 0 ? 0 : d0 / 2 - 1;
   const int npr = d0 / 2 + CB_R / 2 - pr0;
   const int npx = aown * H1, nmt = (npx + 15) / 16;
-  // W2^T hi / lo once per workgroup: item (tap, chunk, ci) gathers co 8 chunk .. + 7
-  for (int e = tid; e < 9 * 8 * C1; e += FT) {
-    const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = w2[(8 * c + u) * 288 + tap * 32 + ci];
-    bf16x8 h, l;
-    split8(v, h, l);
-    *reinterpret_cast<bf16x8*>(smem + XB_WH + xw_off(tap, ci, c)) = h;
-    *reinterpret_cast<bf16x8*>(smem + XB_WL + xw_off(tap, ci, c)) = l;
-  }
+  // W2^T hi / lo planes once per workgroup: the forward wrote them split in this layout
+  for (int i = tid; i < 2 * W2X_PLANE / 16; i += FT)
+    reinterpret_cast<uint4*>(smem + XB_WH)[i] = reinterpret_cast<const uint4*>(w2x)[i];
   // wgrad: this wave's co tile and (tap, ci tile) columns; per-lane tr-read pieces, image
   // independent, so computed once: k-step ks covers run v = 4 ks + g = 8 pixels of output
   // row v / 3 from column 8 (v % 3); the lane addresses pixels col0 + q (+ 4), columns
@@ -944,17 +957,14 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     for (int i = tid; i < 2 * XB_DP / 16; i += FT)
       reinterpret_cast<uint4*>(smem + XB_DH)[i] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = tid; i < (CB_R + 4) * IMG; i += FT) xs[i] = xng[(int64_t)img * 784 + d0 * IMG + i];
-    for (int i = tid; i < (CB_R + 2) * H1 * 4; i += FT) {
-      const int p = i >> 2, c = i & 3;
-      const float4* s4 = reinterpret_cast<const float4*>(
-          a1g + ((int64_t)img * P1 + d0 * H1 + p) * C1 + 8 * c);
-      const float4 u0 = s4[0], u1 = s4[1];
-      const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      bf16x8 h, l;
-      split8(v, h, l);
-      const int off = a1_off(p / H1, p % H1, 16 * c);
-      *reinterpret_cast<bf16x8*>(smem + XB_AH + off) = h;
-      *reinterpret_cast<bf16x8*>(smem + XB_AL + off) = l;
+    {
+      // a1 rows [d0, d0 + 6) of both planes (the forward's split, same swizzled layout)
+      const char* src = a1x + (int64_t)img * 2 * A1X_PLANE + d0 * H1 * 64;
+      for (int i = tid; i < 2 * XB_AP / 16; i += FT) {
+        const int pl = i >= XB_AP / 16, k = i - pl * (XB_AP / 16);
+        reinterpret_cast<uint4*>(smem + XB_AH + pl * XB_AP)[k] =
+            reinterpret_cast<const uint4*>(src + pl * A1X_PLANE)[k];
+      }
     }
     __syncthreads();
     // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
@@ -1083,14 +1093,16 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
                     StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
-                    int32_t* ylab, bool x3, hipStream_t st) {
+                    int32_t* ylab, bool x3, float* w2x, hipStream_t st) {
   if (x3) {
+    // a1g holds the split a1 planes (same bytes as the fp32 a1), w2x the split W2^T planes
     if (a1g != nullptr)
       f32x3_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2, pool,
-                                               pmask, a1g, xng, ylab);
+                                               pmask, reinterpret_cast<char*>(a1g), xng, ylab,
+                                               reinterpret_cast<char*>(w2x));
     else
       f32x3_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2,
-                                                pool, pmask, a1g, xng, ylab);
+                                                pool, pmask, nullptr, xng, ylab, nullptr);
     return;
   }
   if (a1g != nullptr)
@@ -1122,10 +1134,11 @@ int f32_conv_bwd_blocks(int B, int ipb) { return ((B + ipb - 1) / ipb) * CB_S; }
 
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
                          const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
-                         bool x3, hipStream_t st) {
+                         bool x3, const float* w2x, hipStream_t st) {
   if (x3) {
-    f32x3_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(a1g, xng, dpool, pmask, w2,
-                                                                       B, ipb, slab);
+    f32x3_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(
+        reinterpret_cast<const char*>(a1g), xng, dpool, pmask, reinterpret_cast<const char*>(w2x),
+        B, ipb, slab);
     return;
   }
   f32_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(a1g, xng, dpool, pmask, w2, B,

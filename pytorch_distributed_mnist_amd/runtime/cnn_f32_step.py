@@ -58,7 +58,11 @@ class CnnStepF32(GpuStepBase):
         cap = max(B, EVAL_CHUNK)
         self.pool = torch.empty(cap * 9216, dtype=f32, device=dev)
         self.pmask = torch.empty(B * 9216, dtype=torch.uint8, device=dev)
+        # conv1 activations for the backward: fp32, or (split-bf16 mode) the hi / lo bf16
+        # planes in the backward's LDS layout -- the same bytes
         self.a1g = torch.empty(B * 676 * 32, dtype=f32, device=dev)
+        # split-bf16 mode: the W2^T hi / lo planes the forward writes for the backward
+        self.w2x = torch.empty(2 * 9 * 32 * 128 // 4, dtype=f32, device=dev)
         self.xng = torch.empty(B * 784, dtype=f32, device=dev)
         self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
         part_n = max(SPLITK_TRAIN * B, splitk_eval(EVAL_CHUNK) * EVAL_CHUNK) * 128
@@ -127,7 +131,7 @@ class CnnStepF32(GpuStepBase):
         C.f32_fwd(self.ep_images.view(-1, 784), self.ep_labels, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
                   self.pool, self.pmask, self.a1g, self.xng, self.ylab, spe=self.spe,
-                  x3=self.conv_x3)
+                  x3=self.conv_x3, w2x=self.w2x)
         C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN, x3=self.conv_x3)
         C.cnn_head(self.part, SPLITK_TRAIN, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                    self.ylab, True, None, None, ldt, self.head_slab, self.metrics.train_view(),
@@ -139,7 +143,7 @@ class CnnStepF32(GpuStepBase):
         red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
         ipb = conv_ipb(B)
         C.f32_conv_bwd(self.a1g, self.xng, self.dpool, self.pmask, P["conv2.weight"], B,
-                       self.conv_slab, ipb, x3=self.conv_x3)
+                       self.conv_slab, ipb, x3=self.conv_x3, w2x=self.w2x)
         nblk = C.f32_conv_bwd_nblk(B, ipb)
         if self.fuse_conv_reduce:
             self.launch_optimizer(self._fused_segments(nblk))
