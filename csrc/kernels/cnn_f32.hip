@@ -258,7 +258,11 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
   __syncthreads();
   // 2. conv1 + bias + ReLU (exact fp32, VALU): thread = pixel, 8 channels per 16-B chunk of
   // the hi / lo planes
+#if defined(PDM_ABL) && PDM_ABL == 22     // timing ablation only: no conv1
+  for (int p = tid; p < 0; p += FT) {
+#else
   for (int p = tid; p < P1; p += FT) {
+#endif
     const int y = p / H1, x = p - y * H1;
     float xv[9];
 #pragma unroll
@@ -279,7 +283,11 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
       const int off = a1_off(y, x, 16 * c8);
       *reinterpret_cast<bf16x8*>(smem + XF_AH + off) = h;
       *reinterpret_cast<bf16x8*>(smem + XF_AL + off) = l;
+#if defined(PDM_ABL) && PDM_ABL == 21     // timing ablation only: no a1 hand-off writes
+      if (false) {
+#else
       if (TRAIN) {
+#endif
         char* dst = a1x + (int64_t)img * 2 * A1X_PLANE + off;
         *reinterpret_cast<bf16x8*>(dst) = h;
         *reinterpret_cast<bf16x8*>(dst + A1X_PLANE) = l;
@@ -317,7 +325,11 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
   for (int j = 0; j < 2; ++j) b2r[j] = ws[320 + nh * 32 + j * 16 + i16];
   const int pr = wave >> 1;
   const int tt0 = pr < 2 ? 10 * pr : 20 + 8 * (pr - 2), tt1 = tt0 + (pr < 2 ? 10 : 8);
+#if defined(PDM_ABL) && PDM_ABL == 23     // timing ablation only: no conv2
+  for (int tt = tt0; tt < tt0; ++tt) {
+#else
   for (int tt = tt0; tt < tt1; ++tt) {
+#endif
     const int py = tt / 3, px0 = 4 * (tt - py * 3);
     const int tb = (2 * py * H1 + 2 * px0) * 64;
     f32x4 acc[2];
@@ -949,32 +961,81 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
   for (int j = 0; j < 9; ++j) wacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   float db2p = 0.f;
+  // An image's global inputs (scatter mask bytes + dpool values, loaded unconditionally from
+  // clamped indices; the x rows; the a1 plane rows) are loaded into registers one image
+  // ahead: the next image's loads are issued after this image's staging and land while its
+  // dgrad / wgrad run, so the staging after the next barrier only writes LDS.
+  constexpr int SCI = (3 * HP * C2 + FT - 1) / FT;   // scatter items per thread (<= 5)
+  constexpr int A1Q = (2 * XB_AP / 16 + FT - 1) / FT; // a1 16-B pieces per thread (3)
+  const int nsc = npr * HP * C2;
+  // per-thread element offsets of the prefetched inputs (image independent)
+  int goff[SCI], aoffq[A1Q];
+#pragma unroll
+  for (int u = 0; u < SCI; ++u) {
+    const int it = min(tid + u * FT, nsc - 1), pl = it >> 6, co = it & 63;
+    goff[u] = ((pr0 + pl / HP) * HP + pl % HP) * C2 + co;
+  }
+#pragma unroll
+  for (int u = 0; u < A1Q; ++u) {
+    const int i = min(tid + u * FT, 2 * XB_AP / 16 - 1);
+    const int pl = i >= XB_AP / 16, k = i - pl * (XB_AP / 16);
+    aoffq[u] = pl * A1X_PLANE + 16 * k;
+  }
+  const int xoff = d0 * IMG + min(tid, (CB_R + 4) * IMG - 1);
+  uint32_t smk[SCI];
+  float sv[SCI], xv = 0.f;
+  static_assert(A1Q == 3, "three a1 pieces per thread");
+  uint4 a1q0, a1q1, a1q2;             // (named: an array here went to scratch)
+#define X3_PREFETCH(IMG_)                                                                  \
+  do {                                                                                     \
+    const int64_t ib_ = (int64_t)(IMG_);                                                   \
+    static_for<SCI>([&](auto U) __attribute__((always_inline)) {                          \
+      constexpr int u = decltype(U)::value;                                                \
+      smk[u] = pmask[ib_ * FEAT + goff[u]];                                                \
+      sv[u] = dpool[ib_ * FEAT + goff[u]];                                                 \
+    });                                                                                    \
+    xv = xng[ib_ * 784 + xoff];                                                            \
+    const char* src_ = a1x + ib_ * 2 * A1X_PLANE + d0 * H1 * 64;                           \
+    a1q0 = *reinterpret_cast<const uint4*>(src_ + aoffq[0]);                               \
+    a1q1 = *reinterpret_cast<const uint4*>(src_ + aoffq[1]);                               \
+    a1q2 = *reinterpret_cast<const uint4*>(src_ + aoffq[2]);                               \
+  } while (0)
+  if (grp * ipb < B) X3_PREFETCH(grp * ipb);
   for (int ii = 0; ii < ipb; ++ii) {
     const int img = grp * ipb + ii;
     if (img >= B) break;                           // workgroup-uniform
     __syncthreads();   // the previous image's reads of dz2 / a1 / x are done
-    // ---- staging: zero dz2 (both planes), x rows, a1 rows split
+    // ---- staging: zero dz2 (both planes), x rows and a1 plane rows from the registers
+#if !defined(PDM_ABL) || PDM_ABL != 13   // timing ablation only (wrong results)
     for (int i = tid; i < 2 * XB_DP / 16; i += FT)
       reinterpret_cast<uint4*>(smem + XB_DH)[i] = make_uint4(0u, 0u, 0u, 0u);
-    for (int i = tid; i < (CB_R + 4) * IMG; i += FT) xs[i] = xng[(int64_t)img * 784 + d0 * IMG + i];
+#endif
+    if (tid < (CB_R + 4) * IMG) xs[tid] = xv;
     {
-      // a1 rows [d0, d0 + 6) of both planes (the forward's split, same swizzled layout)
-      const char* src = a1x + (int64_t)img * 2 * A1X_PLANE + d0 * H1 * 64;
-      for (int i = tid; i < 2 * XB_AP / 16; i += FT) {
-        const int pl = i >= XB_AP / 16, k = i - pl * (XB_AP / 16);
-        reinterpret_cast<uint4*>(smem + XB_AH + pl * XB_AP)[k] =
-            reinterpret_cast<const uint4*>(src + pl * A1X_PLANE)[k];
+      const uint4 qv[3] = {a1q0, a1q1, a1q2};
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int i = tid + u * FT;
+        if (i < 2 * XB_AP / 16) {
+          const int pl = i >= XB_AP / 16, k = i - pl * (XB_AP / 16);
+          reinterpret_cast<uint4*>(smem + XB_AH + pl * XB_AP)[k] = qv[u];
+        }
       }
     }
     __syncthreads();
     // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
-    for (int it = tid; it < npr * HP * C2; it += FT) {
+#if defined(PDM_ABL) && PDM_ABL == 13
+    static_for<0>([&](auto U) __attribute__((always_inline)) {
+#else
+    static_for<SCI>([&](auto U) __attribute__((always_inline)) {
+#endif
+      constexpr int u = decltype(U)::value;
+      const int it = tid + u * FT;
       const int pl = it >> 6, co = it & 63;
       const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
-      const int gi = (py * HP + px) * C2 + co;
-      const uint8_t mk = pmask[(int64_t)img * FEAT + gi];
-      if (mk & 0x80) {
-        const float v = dpool[(int64_t)img * FEAT + gi];
+      const uint32_t mk = smk[u];
+      if (it < nsc && (mk & 0x80)) {
+        const float v = sv[u];
         const int sidx = __builtin_ctz((unsigned)mk & 0xf);
         const int lr = 2 * py + (sidx >> 1) - (d0 - 2);
         const int zp = 2 + lr * H1 + 2 * px + (sidx & 1);
@@ -984,10 +1045,15 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
         *reinterpret_cast<bf16*>(smem + XB_DL + o) = to_bf16(v - from_bf16(h));
         if (py >= d0 / 2) db2p += v;
       }
-    }
+    });
+    if (ii + 1 < ipb && img + 1 < B) X3_PREFETCH(img + 1);   // lands under this image's compute
     __syncthreads();
     // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
+#if defined(PDM_ABL) && PDM_ABL == 11
+    for (int mt = wave; mt < 0; mt += 8) {
+#else
     for (int mt = wave; mt < nmt; mt += 8) {
+#endif
       const int p = min(mt * 16 + i16, npx - 1);
       const int y = p / H1, x = p - y * H1;
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -1040,6 +1106,9 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
     // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
     // the addresses of pixels col0 + q and col0 + 4 + q of that run, columns 4 pq .. 4 pq + 3
+#if defined(PDM_ABL) && PDM_ABL == 12
+    if (npx < 0)
+#endif
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) {
       const bf16x8 ah = cat_tr(lds_tr16(smem + XB_DH + dza[ks][0]), lds_tr16(smem + XB_DH + dza[ks][1]));
@@ -1087,6 +1156,8 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     else out[SLB_DB1 + ci] = sacc;
   }
 }
+
+#undef X3_PREFETCH
 
 }  // namespace
 
