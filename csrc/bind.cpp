@@ -724,7 +724,7 @@ void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int
 
 void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int64_t B,
                  at::Tensor gwf1, at::Tensor dpool, at::Tensor head_slab, at::Tensor gwf2,
-                 at::Tensor gbf2, at::Tensor gbf1, at::Tensor metrics) {
+                 at::Tensor gbf2, at::Tensor gbf1, at::Tensor metrics, bool x3) {
   c10::DeviceGuard g(dh.device());
   TORCH_CHECK(B >= 1 && ldt % 32 == 0 && ldt >= B, "ldt must be a multiple of 32 and >= B");
   need_min(dh, at::kFloat, ldt * CNN_HID, "dh32");
@@ -746,7 +746,7 @@ void f32_fc1_bwd(at::Tensor dh, int64_t ldt, at::Tensor pool, at::Tensor w1, int
   launch_f32_fc1_bwd(dh.data_ptr<float>(), (int)ldt, pool.data_ptr<float>(), w1.data_ptr<float>(),
                      (int)B, gwf1.data_ptr<float>(), dpool.data_ptr<float>(),
                      head_slab.data_ptr<float>(), hb, gwf2.data_ptr<float>(), gbf2.data_ptr<float>(),
-                     gbf1.data_ptr<float>(), metrics.data_ptr<double>(), cur_stream(dh));
+                     gbf1.data_ptr<float>(), metrics.data_ptr<double>(), x3, cur_stream(dh));
 }
 
 void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor pmask, at::Tensor w2,
@@ -846,7 +846,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("x3") = false, py::arg("w2x") = py::none());
   m.def("f32_fc1_fwd", &f32_fc1_fwd, py::arg("pool"), py::arg("w1"), py::arg("part"), py::arg("B"),
         py::arg("splitk"), py::arg("x3") = false);
-  m.def("f32_fc1_bwd", &f32_fc1_bwd);
+  m.def("f32_fc1_bwd", &f32_fc1_bwd, py::arg("dh"), py::arg("ldt"), py::arg("pool"), py::arg("w1"),
+        py::arg("B"), py::arg("gwf1"), py::arg("dpool"), py::arg("head_slab"), py::arg("gwf2"),
+        py::arg("gbf2"), py::arg("gbf1"), py::arg("metrics"), py::arg("x3") = false);
   m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1,
         py::arg("x3") = false, py::arg("w2x") = py::none());

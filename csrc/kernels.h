@@ -230,7 +230,7 @@ void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, 
                         bool x3, hipStream_t st);
 void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
                         float* gwf1, float* dpool, const float* head_slab, int head_blocks,
-                        float* gwf2, float* gbf2, float* gbf1, double* metrics, hipStream_t st);
+                        float* gwf2, float* gbf2, float* gbf1, double* metrics, bool x3, hipStream_t st);
 // conv backward: (image group of ipb images, row band) workgroups, one slab each
 int f32_conv_bwd_blocks(int B, int ipb);
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,

@@ -545,6 +545,11 @@ constexpr int DX_T = FEAT / DXF;        // 36 per 32 rows
 constexpr int HRB = (HEAD_SLAB + 63) / 64;   // head-slab reduction workgroups (23)
 constexpr int DHP = 144, PTP = 80, DXP = 132, WTP = 272;   // padded LDS row strides (floats)
 
+__device__ __forceinline__ void head_slab_reduce(float* sm, int hb, const float* __restrict__ head_slab,
+                                                 int head_blocks, int B, float* __restrict__ gwf2,
+                                                 float* __restrict__ gbf2, float* __restrict__ gbf1,
+                                                 double* __restrict__ metrics);
+
 __global__ __launch_bounds__(256) void f32_fc1_bwd_kernel(
     const float* __restrict__ dh, int ldt, const float* __restrict__ pool,
     const float* __restrict__ w1, int B, float* __restrict__ gwf1, float* __restrict__ dpool,
@@ -656,11 +661,20 @@ __global__ __launch_bounds__(256) void f32_fc1_bwd_kernel(
       }
     return;
   }
-  // ---- head-slab reduction: 64 slab columns x 4 groups per workgroup, fixed order
+  head_slab_reduce(sm, bid - DW_T - nd, head_slab, head_blocks, B, gwf2, gbf2, gbf1, metrics);
+}
+
+// head-slab reduction (fc1_bwd's third role, both product modes): 64 slab columns x 4 groups
+// per workgroup, fixed order
+__device__ __forceinline__ void head_slab_reduce(float* sm, int hb, const float* __restrict__ head_slab,
+                                                 int head_blocks, int B, float* __restrict__ gwf2,
+                                                 float* __restrict__ gbf2, float* __restrict__ gbf1,
+                                                 double* __restrict__ metrics) {
+  const int tid = threadIdx.x;
   {
     float* rs = sm;
     double* rd = reinterpret_cast<double*>(sm + 256);
-    const int e = (bid - DW_T - nd) * 64 + (tid & 63), grp = tid >> 6;
+    const int e = hb * 64 + (tid & 63), grp = tid >> 6;
     const int ec = min(e, HEAD_SLAB - 1);
     float sacc = 0.f;
     double sd = 0.0;
@@ -688,6 +702,183 @@ __global__ __launch_bounds__(256) void f32_fc1_bwd_kernel(
       else metrics[1] += sd;
     }
   }
+}
+
+// ------------------------------------------------------------------ f32x3_fc1_bwd
+// f32_fc1_bwd's dW and dX roles on split-bf16 products (same grid, same head-slab role).
+// Operands are staged as hi / lo bf16 planes in row-major LDS images and the transposed
+// operands are read with ds_read_b64_tr_b16 (lane 4q + p of a 16-lane group gives row q,
+// columns 4p .. 4p + 3; lane i receives column i); the 32-B column chunk of row r is
+// XOR-swizzled so the eight rows {0..3, 8..11} one 32-lane half reads hit distinct banks.
+// The next chunk's global operands are loaded into registers under the current chunk's
+// MFMAs.
+//   dW tile (64 features, all 128 n), K = batch in chunks of 32 rows:
+//     A = dh^T  (m = n, k = b): tr reads of the dh planes [32 b][128 n]   (256 B rows)
+//     B = pool  (k = b, n = f): tr reads of the pool planes [32 b][64 f]  (128 B rows)
+//   dX tile (32 rows x 256 features), K = 128 n in chunks of 32:
+//     A = dh    (m = b, k = n): ds_read_b128 of the dh planes [32 b][128 n] (272 B rows)
+//     B = W1    (k = n, n = f): tr reads of the W1 planes [32 n][256 f]   (512 B rows)
+__device__ __forceinline__ int sw8(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int sw4(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+// byte offset of element (row r, col c) in a bf16 plane of 256 B / 512 B rows (32-B chunks
+// c / 16 XOR sw8(r)) or of 128 B rows (chunk XOR sw4(r))
+__device__ __forceinline__ int pl256(int r, int c) { return r * 256 + (((c >> 4) ^ sw8(r)) << 5) + 2 * (c & 15); }
+__device__ __forceinline__ int pl512(int r, int c) { return r * 512 + (((c >> 4) ^ sw8(r)) << 5) + 2 * (c & 15); }
+__device__ __forceinline__ int pl128(int r, int c) { return r * 128 + (((c >> 4) ^ sw4(r)) << 5) + 2 * (c & 15); }
+
+constexpr int X1W_DH = 0, X1W_DL = 32 * 256, X1W_PH = 2 * 32 * 256, X1W_PL = X1W_PH + 32 * 128;
+constexpr int X1X_DP = 272;                                  // dX: dh plane row pitch
+constexpr int X1X_DH = 0, X1X_DL = 32 * X1X_DP, X1X_WH = 2 * 32 * X1X_DP, X1X_WL = X1X_WH + 32 * 512;
+constexpr int X1_TOTAL = X1X_WL + 32 * 512;                  // 50176 B (dX; dW uses 24 KB)
+
+__global__ __launch_bounds__(256) void f32x3_fc1_bwd_kernel(
+    const float* __restrict__ dh, int ldt, const float* __restrict__ pool,
+    const float* __restrict__ w1, int B, float* __restrict__ gwf1, float* __restrict__ dpool,
+    const float* __restrict__ head_slab, int head_blocks, float* __restrict__ gwf2,
+    float* __restrict__ gbf2, float* __restrict__ gbf1, double* __restrict__ metrics) {
+  __shared__ __attribute__((aligned(16))) char smc[X1_TOTAL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15, q = (lane >> 2) & 3, pq = lane & 3;
+  const int nd = (ldt / 32) * DX_T;
+  const int bid = blockIdx.x;
+  if (bid < DW_T) {
+    // ---- dW1[n][k0 + f] = sum_b dh[b][n] pool[b][k0 + f]
+    const int k0 = bid * DWF;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // per thread: dh float4 pieces e = tid + 256 u (row e >> 5, cols 4 (e & 31) ..), pool
+    // pieces e = tid + 256 u (row e >> 4, cols 4 (e & 15) ..); rows >= B of pool are zero
+    float4 dv[4], pv[2];
+    auto load = [&](int c0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = tid + 256 * u, r = e >> 5, c4 = e & 31;
+        dv[u] = *reinterpret_cast<const float4*>(dh + (int64_t)(c0 + r) * HID + 4 * c4);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, r = e >> 4, c4 = e & 15;
+        const float4 v = *reinterpret_cast<const float4*>(pool + (int64_t)min(c0 + r, B - 1) * FEAT + k0 + 4 * c4);
+        pv[u] = (c0 + r < B) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    };
+    load(0);
+    for (int c0 = 0; c0 < ldt; c0 += 32) {
+      __syncthreads();   // the previous chunk's reads are done
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = tid + 256 * u, r = e >> 5, c4 = e & 31;
+        const int o = pl256(r, 4 * c4);
+        split4_store(smc + X1W_DH + o, smc + X1W_DL + o, dv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, r = e >> 4, c4 = e & 15;
+        const int o = pl128(r, 4 * c4);
+        split4_store(smc + X1W_PH + o, smc + X1W_PL + o, pv[u]);
+      }
+      __syncthreads();
+      if (c0 + 32 < ldt) load(c0 + 32);   // lands under this chunk's MFMAs
+      // A: rows b = 8 g + q (+ 4), columns n = 32 wave + 16 mt + 4 pq; B: rows b, columns
+      // f = 16 nt + 4 pq
+      bf16x8 ah[2], al[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int c = 32 * wave + 16 * mt + 4 * pq;
+        const int o0 = pl256(8 * g + q, c), o1 = pl256(8 * g + 4 + q, c);
+        ah[mt] = cat_tr(lds_tr16(smc + X1W_DH + o0), lds_tr16(smc + X1W_DH + o1));
+        al[mt] = cat_tr(lds_tr16(smc + X1W_DL + o0), lds_tr16(smc + X1W_DL + o1));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int c = 16 * nt + 4 * pq;
+        const int o0 = pl128(8 * g + q, c), o1 = pl128(8 * g + 4 + q, c);
+        const bf16x8 bh = cat_tr(lds_tr16(smc + X1W_PH + o0), lds_tr16(smc + X1W_PH + o1));
+        const bf16x8 bl = cat_tr(lds_tr16(smc + X1W_PL + o0), lds_tr16(smc + X1W_PL + o1));
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) acc[mt][nt] = mfma3(ah[mt], al[mt], bh, bl, acc[mt][nt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wave * 32 + mt * 16 + 4 * g + r;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + nt * 16 + i16] = acc[mt][nt][r];
+      }
+    return;
+  }
+  if (bid < DW_T + nd) {
+    // ---- dpool[b][f] = sum_n dh[b][n] W1[n][f]: 32 rows x 256 f; wave: 64 f x 32 rows
+    const int t = bid - DW_T;
+    const int b0 = (t / DX_T) * 32, f0 = (t - (t / DX_T) * DX_T) * DXF;
+    float4 wv[8];
+    auto loadw = [&](int n0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {   // W1 chunk: 32 n x 64 float4
+        const int e = tid + 256 * u, r = e >> 6, c4 = e & 63;
+        wv[u] = *reinterpret_cast<const float4*>(w1 + (int64_t)(n0 + r) * FEAT + f0 + 4 * c4);
+      }
+    };
+    loadw(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {     // dh rows b0 .. b0 + 31 (rows >= B are zero)
+      const int e = tid + 256 * u, r = e >> 5, c4 = e & 31;
+      const float4 v = *reinterpret_cast<const float4*>(dh + (int64_t)(b0 + r) * HID + 4 * c4);
+      const int o = r * X1X_DP + 8 * c4;
+      split4_store(smc + X1X_DH + o, smc + X1X_DL + o, v);
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n0 = 0; n0 < HID; n0 += 32) {
+      __syncthreads();   // the previous chunk's W1 reads are done
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = tid + 256 * u, r = e >> 6, c4 = e & 63;
+        const int o = pl512(r, 4 * c4);
+        split4_store(smc + X1X_WH + o, smc + X1X_WL + o, wv[u]);
+      }
+      __syncthreads();
+      if (n0 + 32 < HID) loadw(n0 + 32);
+      bf16x8 ah[2], al[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int o = (mt * 16 + i16) * X1X_DP + (n0 + 8 * g) * 2;
+        ah[mt] = *reinterpret_cast<const bf16x8*>(smc + X1X_DH + o);
+        al[mt] = *reinterpret_cast<const bf16x8*>(smc + X1X_DL + o);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int c = wave * 64 + nt * 16 + 4 * pq;
+        const int o0 = pl512(8 * g + q, c), o1 = pl512(8 * g + 4 + q, c);
+        const bf16x8 bh = cat_tr(lds_tr16(smc + X1X_WH + o0), lds_tr16(smc + X1X_WH + o1));
+        const bf16x8 bl = cat_tr(lds_tr16(smc + X1X_WL + o0), lds_tr16(smc + X1X_WL + o1));
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) acc[mt][nt] = mfma3(ah[mt], al[mt], bh, bl, acc[mt][nt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rowi = b0 + mt * 16 + 4 * g + r;
+        if (rowi < B) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            dpool[(int64_t)rowi * FEAT + f0 + wave * 64 + nt * 16 + i16] = acc[mt][nt][r];
+        }
+      }
+    return;
+  }
+  head_slab_reduce(reinterpret_cast<float*>(smc), bid - DW_T - nd, head_slab, head_blocks, B, gwf2,
+                   gbf2, gbf1, metrics);
 }
 
 // ------------------------------------------------------------------ f32_conv_bwd
@@ -1195,8 +1386,14 @@ void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, 
 
 void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,
                         float* gwf1, float* dpool, const float* head_slab, int head_blocks,
-                        float* gwf2, float* gbf2, float* gbf1, double* metrics, hipStream_t st) {
+                        float* gwf2, float* gbf2, float* gbf1, double* metrics, bool x3,
+                        hipStream_t st) {
   const int nblk = DW_T + (ldt / 32) * DX_T + HRB;
+  if (x3) {
+    f32x3_fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, ldt, pool, w1, B, gwf1, dpool, head_slab,
+                                               head_blocks, gwf2, gbf2, gbf1, metrics);
+    return;
+  }
   f32_fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, ldt, pool, w1, B, gwf1, dpool, head_slab,
                                            head_blocks, gwf2, gbf2, gbf1, metrics);
 }

@@ -80,7 +80,7 @@ class CnnStepF32(GpuStepBase):
                                           "fc2.bias")}
         self.G = {n: a.grad(n) for n in self.P}
         self.fuse_conv_reduce = not self.reducer.active
-        # conv2 and fc1-forward products (the step's FLOPs): "x3" (default) = split-bf16 on the bf16 MFMA
+        # conv2 and fc1 products (the step's FLOPs): "x3" (default) = split-bf16 on the bf16 MFMA
         # (hi.hi + hi.lo + lo.hi, fp32 accumulation; cnn_f32.hip f32x3_*): 4.5e-6 relative
         # error on a conv2 output against fp64, where exact fp32 gives 1.6e-7 and TF32 --
         # cuDNN's default for fp32 convolutions -- 2.9e-4 (tests/test_split_bf16.py); the
@@ -138,7 +138,7 @@ class CnnStepF32(GpuStepBase):
                    self.ctr[0:1], self.opt._step_dev, None, self.dh32)
         C.f32_fc1_bwd(self.dh32, ldt, self.pool, P["fc1.weight"], B, G["fc1.weight"], self.dpool,
                       self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
-                      self.metrics.train_view())
+                      self.metrics.train_view(), x3=self.conv_x3)
         red = self.reducer
         red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
         ipb = conv_ipb(B)
