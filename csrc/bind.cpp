@@ -460,7 +460,8 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
 void fc1_fwd(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_t splitk) {
   c10::DeviceGuard g(pool.device());
   TORCH_CHECK(B >= 1, "B must be >= 1");
-  TORCH_CHECK(splitk >= 1 && 32 % splitk == 0, "splitk must divide 32");
+  TORCH_CHECK(splitk >= 1 && (32 % splitk == 0 || 96 % splitk == 0),
+              "splitk must divide 32 or 96");
   need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
   need_min(wf1, at::kBFloat16, (int64_t)CNN_HID * CNN_FEAT, "wf1");
   need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
@@ -782,6 +783,7 @@ at::Tensor read_stamps(const std::string& which) {
   if (which == "fwd") read_stamps_fwd(p);
   else if (which == "fwd_band") read_stamps_fwd_band(p);
   else if (which == "bwd_band") read_stamps_bwd_band(p);
+  else if (which == "f32") read_stamps_f32(p);
   else read_stamps_bwd(p);
   return t;
 }

@@ -242,3 +242,4 @@ void read_stamps_fwd(unsigned long long* host);
 void read_stamps_bwd(unsigned long long* host);
 void read_stamps_fwd_band(unsigned long long* host);
 void read_stamps_bwd_band(unsigned long long* host);
+void read_stamps_f32(unsigned long long* host);

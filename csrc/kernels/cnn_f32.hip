@@ -218,6 +218,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     float* __restrict__ pool, uint8_t* __restrict__ pmask, char* __restrict__ a1x,
     float* __restrict__ xng, int32_t* __restrict__ ylab, char* __restrict__ w2x) {
   __shared__ __attribute__((aligned(16))) char smem[XF_TOTAL];
+  PDM_STAMP(0);
   float* xs = reinterpret_cast<float*>(smem + XF_XS);
   float* ws = reinterpret_cast<float*>(smem + XF_WS);
   const int img = blockIdx.x;
@@ -255,7 +256,31 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
       const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
       split8(v, bh[t][j], bl[t][j]);
     }
+  // Pin the split here, ahead of conv1: left to the compiler it sinks below conv1, and the
+  // vmcnt(0) it then needs for these loads also waits out every a1 hand-off store conv1 has
+  // issued (gfx9 vmcnt counts stores): ~4 us of the whole chip's 22 MB of writes per launch
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(bh[t][j]), "+v"(bl[t][j]));
+  if (TRAIN) {
+    // W2^T planes for the backward: chunk (tap, c, ci) = co 8 c .. 8 c + 7 of (tap, ci);
+    // ahead of conv1 for the same reason (its loads' vmcnt wait)
+    for (int e = img * FT + tid; e < 9 * 8 * C1; e += gridDim.x * FT) {
+      const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = w2[(8 * c + u) * 288 + tap * 32 + ci];
+      bf16x8 h, l;
+      split8(v, h, l);
+      const int o = (tap * C1 + ci) * 128 + ((c ^ (ci & 7)) << 4);
+      *reinterpret_cast<bf16x8*>(w2x + o) = h;
+      *reinterpret_cast<bf16x8*>(w2x + W2X_PLANE + o) = l;
+    }
+  }
+  PDM_STAMP(1);
   __syncthreads();
+  PDM_STAMP(2);
   // 2. conv1 + bias + ReLU (exact fp32, VALU): thread = pixel, 8 channels per 16-B chunk of
   // the hi / lo planes
 #if defined(PDM_ABL) && PDM_ABL == 22     // timing ablation only: no conv1
@@ -294,21 +319,9 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
       }
     }
   }
-  if (TRAIN) {
-    // W2^T planes for the backward: chunk (tap, c, ci) = co 8 c .. 8 c + 7 of (tap, ci)
-    for (int e = img * FT + tid; e < 9 * 8 * C1; e += gridDim.x * FT) {
-      const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = w2[(8 * c + u) * 288 + tap * 32 + ci];
-      bf16x8 h, l;
-      split8(v, h, l);
-      const int o = (tap * C1 + ci) * 128 + ((c ^ (ci & 7)) << 4);
-      *reinterpret_cast<bf16x8*>(w2x + o) = h;
-      *reinterpret_cast<bf16x8*>(w2x + W2X_PLANE + o) = l;
-    }
-  }
+  PDM_STAMP(3);
   __syncthreads();
+  PDM_STAMP(4);
   // 3. conv2 implicit GEMM (cnn_fwd's tiling): wave pair pr takes tiles [tt0, tt1), the wave
   // its co half nh; lane (g, i16 = 4 q + s) reads pixel (2 py + (s >> 1) + ky,
   // 2 px0 + 2 q + (s & 1) + kx), channels 8 g .. 8 g + 7 (swizzled chunk, per-lane constant)
@@ -325,30 +338,37 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
   for (int j = 0; j < 2; ++j) b2r[j] = ws[320 + nh * 32 + j * 16 + i16];
   const int pr = wave >> 1;
   const int tt0 = pr < 2 ? 10 * pr : 20 + 8 * (pr - 2), tt1 = tt0 + (pr < 2 ? 10 : 8);
+  // Software-pipelined over taps: the A hi / lo reads of the next tap (or of the next tile's
+  // tap 0) are issued, pinned by a scheduling barrier, before this tap's 6 MFMAs.  Left to the
+  // scheduler (the 144 B-fragment registers leave little room) every read waited right in
+  // front of its MFMAs, exposing the LDS latency 18 times per tile.
+  auto tile_base = [&](int tt) {
+    const int py = tt / 3, px0 = 4 * (tt - py * 3);
+    return (2 * py * H1 + 2 * px0) * 64;
+  };
+  bf16x8 ch = *reinterpret_cast<const bf16x8*>(smem + XF_AH + tile_base(tt0) + aoff[0]);
+  bf16x8 cl = *reinterpret_cast<const bf16x8*>(smem + XF_AL + tile_base(tt0) + aoff[0]);
 #if defined(PDM_ABL) && PDM_ABL == 23     // timing ablation only: no conv2
   for (int tt = tt0; tt < tt0; ++tt) {
 #else
   for (int tt = tt0; tt < tt1; ++tt) {
 #endif
     const int py = tt / 3, px0 = 4 * (tt - py * 3);
-    const int tb = (2 * py * H1 + 2 * px0) * 64;
+    const int tb = tile_base(tt), nb = tile_base(min(tt + 1, tt1 - 1));
     f32x4 acc[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[j] = f32x4{b2r[j], b2r[j], b2r[j], b2r[j]};
+    static_for<9>([&](auto T) __attribute__((always_inline)) {
+      constexpr int t = T;
+      const int na = t < 8 ? tb + aoff[t < 8 ? t + 1 : 0] : nb + aoff[0];
+      const bf16x8 xh = *reinterpret_cast<const bf16x8*>(smem + XF_AH + na);
+      const bf16x8 xl = *reinterpret_cast<const bf16x8*>(smem + XF_AL + na);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int t3 = 0; t3 < 9; t3 += 3) {
-      bf16x8 ah[3], al[3];
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        ah[u] = *reinterpret_cast<const bf16x8*>(smem + XF_AH + tb + aoff[t3 + u]);
-        al[u] = *reinterpret_cast<const bf16x8*>(smem + XF_AL + tb + aoff[t3 + u]);
-      }
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[j] = mfma3(ah[u], al[u], bh[t3 + u][j], bl[t3 + u][j], acc[j]);
-    }
+      for (int j = 0; j < 2; ++j) acc[j] = mfma3(ch, cl, bh[t][j], bl[t][j], acc[j]);
+      ch = xh;
+      cl = xl;
+    });
     // epilogue (f32_fwd's): lane's 4 accumulators = the 2x2 window of pooled pixel px0 + g
     const int pp = py * HP + px0 + g;
 #pragma unroll
@@ -367,6 +387,8 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
       if (TRAIN) pmask[(int64_t)img * FEAT + pp * C2 + co] = (uint8_t)(pos ? 0x80u | oh : 0u);
     }
   }
+  PDM_STAMP(5);
+  if (tid == 7 * 64) PDM_STAMP_VAL(6, PDM_CLOCK());
 }
 
 // ------------------------------------------------------------------ f32_fc1_fwd
@@ -1106,11 +1128,16 @@ __device__ __forceinline__ int xw_off(int tap, int ci, int chunk) {
   return (tap * C1 + ci) * 128 + ((chunk ^ (ci & 7)) << 4);
 }
 
+struct DgFrag {   // one dgrad k-step's operands: dz2 hi / lo rows, W2^T hi / lo of 2 ci tiles
+  bf16x8 ah, al, bh[2], bl[2];
+};
+
 __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     const char* __restrict__ a1x, const float* __restrict__ xng, const float* __restrict__ dpool,
     const uint8_t* __restrict__ pmask, const char* __restrict__ w2x, int B, int ipb,
     float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) char smem[XB_TOTAL];
+  PDM_STAMP(8);
   float* xs = reinterpret_cast<float*>(smem + XB_XS);
   const int grp = blockIdx.x / CB_S, band = blockIdx.x - grp * CB_S;
   const int d0 = band * CB_R;
@@ -1130,6 +1157,9 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
   // row v / 3 from column 8 (v % 3); the lane addresses pixels col0 + q (+ 4), columns
   // 4 pq .. 4 pq + 3.  a1 pixel (r + ky, col0 + q + kx (+ 4)): col0 % 8 == 0, so the a1_off
   // swizzle term depends on (q + kx) & 3 only -> a base per k-step + a constant per tap
+  // dgrad W2^T fragment bases (xw_off with ci & 7 == i16 & 7) for k-halves kk = 0, 1
+  const int wbase0 = XB_WH + i16 * 128 + ((g ^ (i16 & 7)) << 4);
+  const int wbase1 = XB_WH + i16 * 128 + (((4 + g) ^ (i16 & 7)) << 4);
   const int wmt = wave & 3, wn0 = 9 * (wave >> 2);
   const int q = (lane >> 2) & 3, pq = lane & 3;
   int dza[3][2], a1b[3], a1s[3][2];
@@ -1192,6 +1222,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     a1q2 = *reinterpret_cast<const uint4*>(src_ + aoffq[2]);                               \
   } while (0)
   if (grp * ipb < B) X3_PREFETCH(grp * ipb);
+  PDM_STAMP(9);
   for (int ii = 0; ii < ipb; ++ii) {
     const int img = grp * ipb + ii;
     if (img >= B) break;                           // workgroup-uniform
@@ -1214,6 +1245,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
       }
     }
     __syncthreads();
+    if (ii == 0) PDM_STAMP(10);
     // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
 #if defined(PDM_ABL) && PDM_ABL == 13
     static_for<0>([&](auto U) __attribute__((always_inline)) {
@@ -1239,6 +1271,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     });
     if (ii + 1 < ipb && img + 1 < B) X3_PREFETCH(img + 1);   // lands under this image's compute
     __syncthreads();
+    if (ii == 0) PDM_STAMP(11);
     // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
 #if defined(PDM_ABL) && PDM_ABL == 11
     for (int mt = wave; mt < 0; mt += 8) {
@@ -1248,27 +1281,37 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
       const int p = min(mt * 16 + i16, npx - 1);
       const int y = p / H1, x = p - y * H1;
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll 1
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap - 3 * ky;
-        const int zp = 2 + (y + 2 - ky) * H1 + x - kx;
-        bf16x8 ah[2], al[2], bh[2][2], bl[2][2];
+      // 18 k-steps (tap, 32-co half kk), software-pipelined: the 6 fragments of step s + 1 are
+      // read (pinned by a scheduling barrier) before step s's 6 MFMAs, double-buffered in
+      // two named sets (a per-step array index would put them in scratch)
+      DgFrag f0, f1;
+      const int zp0 = 2 + (y + 2) * H1 + x;
+      auto dg_load = [&](auto TAP, auto KK, DgFrag& f) __attribute__((always_inline)) {
+        constexpr int tap = decltype(TAP)::value, kk = decltype(KK)::value;
+        constexpr int ky = tap / 3, kx = tap - 3 * ky;
+        const int zp = zp0 - ky * H1 - kx;
+        f.ah = *reinterpret_cast<const bf16x8*>(smem + XB_DH + xdz_off(zp, 4 * kk + g));
+        f.al = *reinterpret_cast<const bf16x8*>(smem + XB_DL + xdz_off(zp, 4 * kk + g));
+        // W2^T rows ci = 16 nt + i16: xw_off = a per-lane base per kk (ci & 7 == i16 & 7) +
+        // a compile-time offset, so no per-(tap, nt) address stays live across the loops
+        const char* wb = smem + (kk ? wbase1 : wbase0);
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          ah[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DH + xdz_off(zp, 4 * kk + g));
-          al[kk] = *reinterpret_cast<const bf16x8*>(smem + XB_DL + xdz_off(zp, 4 * kk + g));
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const int wo = xw_off(tap, nt * 16 + i16, 4 * kk + g);
-            bh[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WH + wo);
-            bl[kk][nt] = *reinterpret_cast<const bf16x8*>(smem + XB_WL + wo);
-          }
+        for (int nt = 0; nt < 2; ++nt) {
+          f.bh[nt] = *reinterpret_cast<const bf16x8*>(wb + (tap * C1 + nt * 16) * 128);
+          f.bl[nt] = *reinterpret_cast<const bf16x8*>(wb + XB_WP + (tap * C1 + nt * 16) * 128);
         }
+      };
+      dg_load(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, f0);
+      static_for<18>([&](auto S) __attribute__((always_inline)) {
+        constexpr int st = decltype(S)::value;
+        DgFrag& cur = st % 2 == 0 ? f0 : f1;
+        DgFrag& nxt = st % 2 == 0 ? f1 : f0;
+        if constexpr (st + 1 < 18)
+          dg_load(std::integral_constant<int, (st + 1) / 2>{}, std::integral_constant<int, (st + 1) % 2>{}, nxt);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma3(ah[kk], al[kk], bh[kk][nt], bl[kk][nt], acc[nt]);
-      }
+        for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma3(cur.ah, cur.al, cur.bh[nt], cur.bl[nt], acc[nt]);
+      });
       float xb[4];
       const int ctap = i16;
 #pragma unroll
@@ -1294,18 +1337,23 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
     }
+    if (ii == 0) PDM_STAMP(12);
     // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
     // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
     // the addresses of pixels col0 + q and col0 + 4 + q of that run, columns 4 pq .. 4 pq + 3
 #if defined(PDM_ABL) && PDM_ABL == 12
     if (npx < 0)
 #endif
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
-      const bf16x8 ah = cat_tr(lds_tr16(smem + XB_DH + dza[ks][0]), lds_tr16(smem + XB_DH + dza[ks][1]));
-      const bf16x8 al = cat_tr(lds_tr16(smem + XB_DL + dza[ks][0]), lds_tr16(smem + XB_DL + dza[ks][1]));
-#pragma unroll
-      for (int j = 0; j < 9; ++j) {
+    {
+      // 27 steps (k-step ks, column j), software-pipelined like the dgrad: the B pieces of
+      // step s + 1 and (two steps before a k-step starts) its A pieces are read, pinned by a
+      // scheduling barrier, before step s's 3 MFMAs; named rotating registers (no arrays; a
+      // second step of B lookahead spilled)
+      auto ld_a = [&](int ks, bf16x8& ah, bf16x8& al) __attribute__((always_inline)) {
+        ah = cat_tr(lds_tr16(smem + XB_DH + dza[ks][0]), lds_tr16(smem + XB_DH + dza[ks][1]));
+        al = cat_tr(lds_tr16(smem + XB_DL + dza[ks][0]), lds_tr16(smem + XB_DL + dza[ks][1]));
+      };
+      auto ld_b = [&](int ks, int j, bf16x8& bh, bf16x8& bl) __attribute__((always_inline)) {
         // (tap, ci tile) of column j: wave-uniform, so ky / kx / ct are per-wave values and
         // the offset below is one add of a per-lane base and a small table entry
         const int nn = wn0 + j, tap = nn >> 1, ct = nn & 1;
@@ -1314,12 +1362,33 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
         const int s2 = ct ? a1s[2][1] : a1s[2][0];
         const int kxs = kx == 0 ? s0 : (kx == 1 ? s1 : s2);   // selects: no indexed registers
         const int o0 = a1b[ks] + (ky * H1 + kx) * 64 + kxs;
-        const bf16x8 bh = cat_tr(lds_tr16(smem + XB_AH + o0), lds_tr16(smem + XB_AH + o0 + 256));
-        const bf16x8 bl = cat_tr(lds_tr16(smem + XB_AL + o0), lds_tr16(smem + XB_AL + o0 + 256));
+        bh = cat_tr(lds_tr16(smem + XB_AH + o0), lds_tr16(smem + XB_AH + o0 + 256));
+        bl = cat_tr(lds_tr16(smem + XB_AL + o0), lds_tr16(smem + XB_AL + o0 + 256));
+      };
+      bf16x8 ah0, al0, ah1, al1, bh0, bl0, bh1, bl1;
+      ld_a(0, ah0, al0);
+      ld_b(0, 0, bh0, bl0);
+      static_for<27>([&](auto S) __attribute__((always_inline)) {
+        constexpr int st = decltype(S)::value, ks = st / 9, j = st % 9;
+        constexpr int sn = st + 1, ksn = sn / 9, jn = sn % 9;
+        bf16x8& bhn = sn % 2 == 0 ? bh0 : bh1;
+        bf16x8& bln = sn % 2 == 0 ? bl0 : bl1;
+        if constexpr (sn < 27) ld_b(ksn, jn, bhn, bln);
+        if constexpr (j == 7 && ks < 2) {
+          if constexpr ((ks + 1) % 2 == 0) ld_a(ks + 1, ah0, al0);
+          else ld_a(ks + 1, ah1, al1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8& ah = ks % 2 == 0 ? ah0 : ah1;
+        const bf16x8& al = ks % 2 == 0 ? al0 : al1;
+        const bf16x8& bh = st % 2 == 0 ? bh0 : bh1;
+        const bf16x8& bl = st % 2 == 0 ? bl0 : bl1;
         wacc[j] = mfma3(ah, al, bh, bl, wacc[j]);
-      }
+      });
     }
+    if (ii == 0) PDM_STAMP(13);
   }
+  PDM_STAMP(14);
   __syncthreads();   // dz2 planes free: reduction scratch
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
@@ -1346,11 +1415,21 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     if (tp < 9) out[SLB_DW1 + ci * 9 + tp] = sacc;
     else out[SLB_DB1 + ci] = sacc;
   }
+  PDM_STAMP(15);
 }
 
 #undef X3_PREFETCH
 
 }  // namespace
+
+// f32x3_fwd stamps in slots 0-6, f32x3_conv_bwd in 8-15 (PDM_STAMPS builds; tools/stamps_f32.py)
+void read_stamps_f32(unsigned long long* host) {
+#ifdef PDM_STAMPS
+  hipMemcpyFromSymbol(host, HIP_SYMBOL(pdm_stamps), sizeof(unsigned long long) * 256 * 16);
+#else
+  for (int i = 0; i < 256 * 16; ++i) host[i] = 0;
+#endif
+}
 
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
                     StepRows sr, int B, const float* w1, const float* b1, const float* w2,

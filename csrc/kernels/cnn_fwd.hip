@@ -284,12 +284,14 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 #endif  // PDM_WANT_FWD_REST
 #if PDM_WANT_FC1_FWD
 // ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
-constexpr int FC1_KB = 9;   // k-steps per load batch (288 k-steps = 32 batches)
-constexpr int FC1_AROW = FC1_KB * 32 * 2 + 32;   // LDS bytes per staged pool row (padded)
-
+// KB = k-steps per load batch: 9 (288 k-steps = 32 batches; split factors dividing 32) or 3
+// (96 batches: split factors up to 96, so B <= 64 can put W1 on ~256 CUs instead of 32-64)
+template <int KB>
 __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
                                                       float* __restrict__ part, int B, int kchunk) {
+  constexpr int FC1_KB = KB;
+  constexpr int FC1_AROW = FC1_KB * 32 * 2 + 32;   // LDS bytes per staged pool row (padded)
   // XCD-aware mapping of the 1-D grid: workgroup w runs on XCD w % 8.  When the split
   // count is a multiple of 8, every XCD owns S/8 splits (1/8 of W1's K range, for all
   // m-tiles), so each XCD's L2 holds only its slice of W1 instead of all of it.
@@ -311,9 +313,9 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
   const int n0 = wave * 32;
   // The pool tile (32 rows x 288 k per batch) is staged once per workgroup through LDS by
   // whole-line loads (it was read by each of the 4 waves, as 16 half lines per load);
-  // rows are padded to 608 B, so the A-fragment reads (16 rows x 16 B per lane group) are
-  // bank-conflict-free (tools/lds_bank_model.py gfx950 ds_read_b128 lane groups: 592 B rows
-  // were 2 passes per read, 40 % conflict cycles in the PMC table).  Rows past B read row
+  // rows are padded by 32 B (608 B / 224 B), so the A-fragment reads (16 rows x 16 B per
+  // lane group) are bank-conflict-free (tools/lds_bank_model.py gfx950 ds_read_b128 lane
+  // groups: 592 B rows were 2 passes per read, 40 % conflict cycles in the PMC table).  Rows past B read row
   // B-1 (valid data, outputs never stored).
   __shared__ __attribute__((aligned(16))) char at[32 * FC1_AROW];
   // W1 is fragment-major (kernels.h frag_pos): the 16 x 32 fragment (n-tile, k-step) is
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int ACH = 32 * FC1_KB * 32 * 2 / 16;   // 16-B chunks of the A tile (1152)
   // K in batches of FC1_KB steps: every operand load of a batch is issued before its
-  // MFMAs (kchunk is a multiple of 32 * FC1_KB: split factors divide 32)
+  // MFMAs (kchunk is a multiple of 32 * FC1_KB: the launch picks KB from the split factor)
   for (int kb = 0; kb < kchunk; kb += 32 * FC1_KB) {
     uint4 av[(ACH + 255) / 256];
 #pragma unroll
@@ -563,7 +565,10 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st) {
   dim3 grid(((B + 31) / 32) * splitk);
-  fc1_fwd_kernel<<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);
+  if (32 % splitk == 0)
+    fc1_fwd_kernel<9><<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);
+  else
+    fc1_fwd_kernel<3><<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);
 }
 
 #endif

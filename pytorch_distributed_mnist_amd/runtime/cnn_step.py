@@ -60,11 +60,11 @@ def frag_major_t(w: torch.Tensor) -> torch.Tensor:
 
 
 def choose_splitk(B: int, cap: int = 32, target_blocks: int = 256) -> int:
-    """Split-K factor for fc1_fwd: a divisor of 32 (so every split holds whole 9-step load
-    batches of the 288 K-steps) giving ~target_blocks workgroups."""
+    """Split-K factor for fc1_fwd giving ~target_blocks workgroups: a divisor of 32 (every
+    split holds whole 9-step load batches of the 288 K-steps) or 48 / 96 (3-step batches)."""
     mtiles = (B + 31) // 32
     best = 1
-    for s in (1, 2, 4, 8, 16, 32):
+    for s in (1, 2, 4, 8, 16, 32, 48, 96):
         if s <= cap and mtiles * s <= target_blocks:
             best = s
     return best

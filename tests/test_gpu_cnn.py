@@ -178,6 +178,25 @@ def test_cnn_forward_kernels(gpu, B):
     assert (((mask & 0x0F) & ((mask & 0x0F) - 1)) == 0).all()   # one bit at most
 
 
+@pytest.mark.parametrize("B,S", [(32, 32), (32, 96), (64, 48), (37, 96), (256, 32)])
+def test_fc1_fwd_split_k(gpu, B, S):
+    """fc1_fwd's split-K partials (9-k-step load batches for S | 32, 3-k-step batches for
+    S = 48 / 96) sum to pool . W1^T of the bf16 operands in fp32."""
+    prog, _, _ = _program(B)
+    st = prog.gpu
+    C = st.C
+    g = torch.Generator().manual_seed(B + S)
+    pool = torch.randn(B, 9216, generator=g).to(torch.bfloat16)
+    w1 = prog.arena.param("fc1.weight").reshape(128, 9216).float().cpu()   # kernel layout
+    part = torch.full((S * B * 128,), float("nan"), device=st.pool.device)
+    C.fc1_fwd(pool.to(st.pool.device), st.wf1, part, B, S)
+    torch.cuda.synchronize()
+    got = part.view(S, B, 128).sum(0).cpu()
+    ref = pool.float() @ bf(w1).t()
+    assert torch.isfinite(got).all()
+    assert rel(got, ref) < 1e-5
+
+
 @pytest.mark.parametrize("B", [64, 40, 300])
 def test_cnn_step_gradients_match_autograd(gpu, B):
     prog, train, _ = _program(B)      # SGD lr=0: params unchanged, grads left in the arena
