@@ -760,7 +760,7 @@ void f32_conv_bwd(at::Tensor a1g, at::Tensor xng, at::Tensor dpool, at::Tensor p
   need_min(pmask, at::kByte, B * CNN_FEAT, "pmask");
   need(w2, at::kFloat, "w2");
   TORCH_CHECK(w2.numel() == 64 * 288, "conv2 weight");
-  need_min(slab, at::kFloat, (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb) * CNN_CONV_SLAB,
+  need_min(slab, at::kFloat, (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb, x3) * CNN_CONV_SLAB,
            "conv slab");
   launch_f32_conv_bwd(a1g.data_ptr<float>(), xng.data_ptr<float>(), dpool.data_ptr<float>(),
                       pmask.data_ptr<uint8_t>(), w2.data_ptr<float>(), (int)B, (int)ipb,
@@ -854,8 +854,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("f32_conv_bwd", &f32_conv_bwd, py::arg("a1g"), py::arg("xng"), py::arg("dpool"),
         py::arg("pmask"), py::arg("w2"), py::arg("B"), py::arg("slab"), py::arg("ipb") = 1,
         py::arg("x3") = false, py::arg("w2x") = py::none());
-  m.def("f32_conv_bwd_nblk", [](int64_t B, int64_t ipb) {
-    return (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb); }, py::arg("B"), py::arg("ipb") = 1);
+  m.def("f32_conv_bwd_nblk", [](int64_t B, int64_t ipb, bool x3) {
+    return (int64_t)f32_conv_bwd_blocks((int)B, (int)ipb, x3); }, py::arg("B"), py::arg("ipb") = 1,
+    py::arg("x3") = false);
   m.def("cnn_bwd_nblk", &cnn_bwd_nblk, py::arg("B"), py::arg("ipb"), py::arg("bands") = 1);
   m.def("read_stamps", &read_stamps);
   m.def("graph_upload", &graph_upload);

@@ -232,7 +232,7 @@ void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float
                         float* gwf1, float* dpool, const float* head_slab, int head_blocks,
                         float* gwf2, float* gbf2, float* gbf1, double* metrics, bool x3, hipStream_t st);
 // conv backward: (image group of ipb images, row band) workgroups, one slab each
-int f32_conv_bwd_blocks(int B, int ipb);
+int f32_conv_bwd_blocks(int B, int per, bool x3);
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
                          const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
                          bool x3, const float* w2x, hipStream_t st);

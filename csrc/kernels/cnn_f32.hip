@@ -208,6 +208,7 @@ constexpr int XF_WS = 3136;                       // fp32 w1 [288] | b1 [32] | b
 constexpr int XF_AH = 4736;                       // bf16 a1 hi plane [676 px][64 B], swizzled
 constexpr int XF_AL = XF_AH + P1 * 64;            // bf16 a1 lo plane
 constexpr int XF_TOTAL = XF_AL + P1 * 64;         // 91264 B
+constexpr int XF_W2R = 292;                       // W2 staging row (floats): 288 + 4 pad
 static_assert(XF_TOTAL <= 163840 && XF_AH % 128 == 0 && XF_AL % 128 == 0, "f32x3_fwd LDS");
 
 template <bool TRAIN>
@@ -242,35 +243,44 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     if (TRAIN) reinterpret_cast<float4*>(xng + (int64_t)img * 784)[tid] = x;
   }
   if (tid == 64) ylab[img] = labels[row];
-  // 1. this wave's conv2 B fragments, split: co = 32 nh + 16 j + i16, k = ci = 8 g .. 8 g + 7
-  // of tap t (W2 internal layout [co][ky][kx][ci]); in flight while conv1 runs
+  // 1. W2 (fp32 [co][tap][ci], 73.7 KB) staged once per workgroup through the a1 planes' LDS
+  // (rows padded to 1168 B): the waves' B fragments were 8 x 36.9 KB of L2 reads per CU,
+  // 75 MB per launch, and the launch's first ~7 us
+  float* w2s = reinterpret_cast<float*>(smem + XF_AH);
+  static_assert(C2 * XF_W2R * 4 <= 2 * P1 * 64, "W2 staging fits the a1 planes");
+#pragma unroll
+  for (int u = 0; u < C2 * 288 / 4 / FT; ++u) {
+    const int e = tid + u * FT, co = e / 72, c4 = e - co * 72;
+    reinterpret_cast<float4*>(w2s + co * XF_W2R)[c4] = reinterpret_cast<const float4*>(w2)[e];
+  }
+  __syncthreads();
+  // this wave's conv2 B fragments, split: co = 32 nh + 16 j + i16, k = ci = 8 g .. 8 g + 7 of
+  // tap t (W2 internal layout [co][ky][kx][ci])
   const int nh = wave & 1;
   bf16x8 bh[9][2], bl[9][2];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const float4* src = reinterpret_cast<const float4*>(
-          w2 + ((int64_t)(nh * 32 + j * 16 + i16) * 9 + t) * 32 + 8 * g);
+      const float4* src = reinterpret_cast<const float4*>(w2s + (nh * 32 + j * 16 + i16) * XF_W2R +
+                                                          t * 32 + 8 * g);
       const float4 p0 = src[0], p1 = src[1];
       const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
       split8(v, bh[t][j], bl[t][j]);
     }
-  // Pin the split here, ahead of conv1: left to the compiler it sinks below conv1, and the
-  // vmcnt(0) it then needs for these loads also waits out every a1 hand-off store conv1 has
-  // issued (gfx9 vmcnt counts stores): ~4 us of the whole chip's 22 MB of writes per launch
+  // pinned here: the compiler would sink the split below conv1 (pressure), where the staging
+  // area is already overwritten
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(bh[t][j]), "+v"(bl[t][j]));
   if (TRAIN) {
-    // W2^T planes for the backward: chunk (tap, c, ci) = co 8 c .. 8 c + 7 of (tap, ci);
-    // ahead of conv1 for the same reason (its loads' vmcnt wait)
+    // W2^T planes for the backward: chunk (tap, c, ci) = co 8 c .. 8 c + 7 of (tap, ci)
     for (int e = img * FT + tid; e < 9 * 8 * C1; e += gridDim.x * FT) {
       const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = w2[(8 * c + u) * 288 + tap * 32 + ci];
+      for (int u = 0; u < 8; ++u) v[u] = w2s[(8 * c + u) * XF_W2R + tap * 32 + ci];
       bf16x8 h, l;
       split8(v, h, l);
       const int o = (tap * C1 + ci) * 128 + ((c ^ (ci & 7)) << 4);
@@ -279,43 +289,76 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     }
   }
   PDM_STAMP(1);
-  __syncthreads();
+  __syncthreads();   // every wave's staging reads are done: conv1 overwrites the area
   PDM_STAMP(2);
-  // 2. conv1 + bias + ReLU (exact fp32, VALU): thread = pixel, 8 channels per 16-B chunk of
-  // the hi / lo planes
-#if defined(PDM_ABL) && PDM_ABL == 22     // timing ablation only: no conv1
-  for (int p = tid; p < 0; p += FT) {
-#else
-  for (int p = tid; p < P1; p += FT) {
-#endif
-    const int y = p / H1, x = p - y * H1;
-    float xv[9];
+  // 2. conv1 + bias + ReLU on the bf16 MFMA, split-bf16 with the three partial products packed
+  // into one K = 32 step: slot k = 9 term + tap (k < 27) holds x_hi.w_hi (term 0), x_lo.w_hi
+  // (1), x_hi.w_lo (2) of tap k % 9, slots 27..31 zero; fp32 accumulation from the bias.
+  // A = weights (row = channel 16 nt + i16), B = 16 "virtual pixels" V = 28 y + x of the
+  // 28-wide x image (x = 26, 27 and y >= 26 computed and dropped; x & 3 == lane & 3), so the
+  // lane's D = 4 consecutive channels 16 nt + 4 g .. + 3 of pixel V: one 8-B store per plane
+  {
+    bf16x8 wa[2];
+    int xo[8];
+    uint32_t lomask = 0;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) xv[t] = xs[(y + t / 3) * IMG + x + t % 3];
-#pragma unroll 1
-    for (int c8 = 0; c8 < C1 / 8; ++c8) {
-      float o[8];
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * g + e, term = k / 9, tap = k - 9 * term;
+      xo[e] = k < 27 ? (tap / 3) * IMG + tap % 3 : 0;
+      lomask |= (term == 1 ? 1u : 0u) << e;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int co = 8 * c8 + u;
-        float acc = ws[288 + co];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) acc = fmaf(ws[co * 9 + t], xv[t], acc);
-        o[u] = fmaxf(acc, 0.f);
+      for (int nt = 0; nt < 2; ++nt) {
+        const float w = ws[(16 * nt + i16) * 9 + tap];
+        const bf16 whi = to_bf16(w);
+        wa[nt][e] = k >= 27 ? to_bf16(0.f) : term == 2 ? to_bf16(w - from_bf16(whi)) : whi;
       }
-      bf16x8 h, l;
-      split8(o, h, l);
-      const int off = a1_off(y, x, 16 * c8);
-      *reinterpret_cast<bf16x8*>(smem + XF_AH + off) = h;
-      *reinterpret_cast<bf16x8*>(smem + XF_AL + off) = l;
-#if defined(PDM_ABL) && PDM_ABL == 21     // timing ablation only: no a1 hand-off writes
-      if (false) {
+    }
+    const uint32_t zmask = g == 3 ? 0xF8u : 0u;   // slots 27..31
+    f32x4 bias[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[nt][r] = ws[288 + 16 * nt + 4 * g + r];
+    const int a1c = (((g >> 1) ^ (i16 & 3)) << 4) + 8 * (g & 1);   // nt = 0; nt = 1: ^ 32
+#if defined(PDM_ABL) && PDM_ABL == 22     // timing ablation only: no conv1
+    for (int tile = wave; tile < 0; tile += 8) {
 #else
-      if (TRAIN) {
+    for (int tile = wave; tile < (IMG * H1 + 15) / 16; tile += 8) {
 #endif
-        char* dst = a1x + (int64_t)img * 2 * A1X_PLANE + off;
-        *reinterpret_cast<bf16x8*>(dst) = h;
-        *reinterpret_cast<bf16x8*>(dst + A1X_PLANE) = l;
+      const int V = tile * 16 + i16;
+      bf16x8 xb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = xs[min(V + xo[e], IMG * IMG - 1)];
+        const bf16 h = to_bf16(v);
+        const bf16 l = to_bf16(v - from_bf16(h));
+        xb[e] = (zmask >> e) & 1 ? to_bf16(0.f) : ((lomask >> e) & 1 ? l : h);
+      }
+      const int y = V / IMG, x = V - y * IMG;
+      const bool ok = y < H1 && x < H1;
+      const int ab = (V - 2 * y) * 64 + a1c;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nt], xb, bias[nt], 0, 0, 0);
+        bf16x4 h, l;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float o = fmaxf(acc[r], 0.f);
+          h[r] = to_bf16(o);
+          l[r] = to_bf16(o - from_bf16(h[r]));
+        }
+        if (ok) {
+          const int off = ab ^ (32 * nt);
+          *reinterpret_cast<bf16x4*>(smem + XF_AH + off) = h;
+          *reinterpret_cast<bf16x4*>(smem + XF_AL + off) = l;
+#if !defined(PDM_ABL) || PDM_ABL != 21     // timing ablation only: no a1 hand-off writes
+          if (TRAIN) {
+            char* dst = a1x + (int64_t)img * 2 * A1X_PLANE + off;
+            *reinterpret_cast<bf16x4*>(dst) = h;
+            *reinterpret_cast<bf16x4*>(dst + A1X_PLANE) = l;
+          }
+#endif
+        }
       }
     }
   }
@@ -462,7 +505,7 @@ __global__ __launch_bounds__(256) void f32_fc1_fwd_kernel(const float* __restric
 constexpr int XK = 3;
 constexpr int XKP = XK * 32 * 2 + 16;             // 208 B
 constexpr int XF_BH = 2 * 32 * XKP, XF_BL = XF_BH + HID * XKP;
-constexpr int XF1_TOTAL = XF_BL + HID * XKP;       // 66560 B: 2 workgroups / CU
+constexpr int XF1_TOTAL = XF_BL + HID * XKP;       // 66560 B
 
 __device__ __forceinline__ void split4_store(char* hi, char* lo, float4 v) {
   const float f[4] = {v.x, v.y, v.z, v.w};
@@ -476,7 +519,7 @@ __device__ __forceinline__ void split4_store(char* hi, char* lo, float4 v) {
   *reinterpret_cast<bf16x4*>(lo) = l;
 }
 
-__global__ __launch_bounds__(256, 2) void f32x3_fc1_fwd_kernel(const float* __restrict__ pool,
+__global__ __launch_bounds__(256, 1) void f32x3_fc1_fwd_kernel(const float* __restrict__ pool,
                                                                const float* __restrict__ w1,
                                                                float* __restrict__ part, int B,
                                                                int kchunk) {
@@ -501,8 +544,10 @@ __global__ __launch_bounds__(256, 2) void f32x3_fc1_fwd_kernel(const float* __re
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int C4 = XK * 8;                        // float4 per staged row (24)
-  for (int kb = 0; kb < kchunk; kb += 32 * XK) {
-    float4 av[3], wv[12];
+  // batch kb + 96's global loads are issued right after batch kb's staging barrier, so they
+  // land under its MFMAs (one workgroup per CU at the training split: registers to spare)
+  float4 av[3], wv[12];
+  auto load = [&](int kb) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 3; ++u) {                   // A: 32 rows x 24 float4 (rows past B clamped)
       const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
@@ -513,6 +558,9 @@ __global__ __launch_bounds__(256, 2) void f32x3_fc1_fwd_kernel(const float* __re
       const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
       wv[u] = *reinterpret_cast<const float4*>(w1 + (int64_t)r * FEAT + kbeg + kb + 4 * c4);
     }
+  };
+  load(0);
+  for (int kb = 0; kb < kchunk; kb += 32 * XK) {
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
       const int e = tid + 256 * u, r = e / C4, c4 = e - r * C4;
@@ -524,6 +572,8 @@ __global__ __launch_bounds__(256, 2) void f32x3_fc1_fwd_kernel(const float* __re
       split4_store(sm + XF_BH + r * XKP + 8 * c4, sm + XF_BL + r * XKP + 8 * c4, wv[u]);
     }
     __syncthreads();
+    if (kb + 32 * XK < kchunk) load(kb + 32 * XK);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < XK; ++ks) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
@@ -1134,21 +1184,17 @@ struct DgFrag {   // one dgrad k-step's operands: dz2 hi / lo rows, W2^T hi / lo
 
 __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     const char* __restrict__ a1x, const float* __restrict__ xng, const float* __restrict__ dpool,
-    const uint8_t* __restrict__ pmask, const char* __restrict__ w2x, int B, int ipb,
+    const uint8_t* __restrict__ pmask, const char* __restrict__ w2x, int B, int upw,
     float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) char smem[XB_TOTAL];
   PDM_STAMP(8);
   float* xs = reinterpret_cast<float*>(smem + XB_XS);
-  const int grp = blockIdx.x / CB_S, band = blockIdx.x - grp * CB_S;
-  const int d0 = band * CB_R;
-  const int aown = band == CB_S - 1 ? CB_R + 2 : CB_R;
+  // units (image, row band), image-major: this workgroup takes [u0, u1)
+  const int u0 = blockIdx.x * upw, u1 = min(u0 + upw, B * CB_S);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;
   float* out = slab + (int64_t)blockIdx.x * CNN_CONV_SLAB;
-  const int pr0 = band == 0 ? 0 : d0 / 2 - 1;
-  const int npr = d0 / 2 + CB_R / 2 - pr0;
-  const int npx = aown * H1, nmt = (npx + 15) / 16;
   // W2^T hi / lo planes once per workgroup: the forward wrote them split in this layout
   for (int i = tid; i < 2 * W2X_PLANE / 16; i += FT)
     reinterpret_cast<uint4*>(smem + XB_WH)[i] = reinterpret_cast<const uint4*>(w2x)[i];
@@ -1182,51 +1228,56 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
   for (int j = 0; j < 9; ++j) wacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   float db2p = 0.f;
-  // An image's global inputs (scatter mask bytes + dpool values, loaded unconditionally from
-  // clamped indices; the x rows; the a1 plane rows) are loaded into registers one image
-  // ahead: the next image's loads are issued after this image's staging and land while its
+  // A unit's global inputs (scatter mask bytes + dpool values, loaded unconditionally from
+  // clamped indices; the x rows; the a1 plane rows) are loaded into registers one unit
+  // ahead: the next unit's loads are issued after this unit's staging and land while its
   // dgrad / wgrad run, so the staging after the next barrier only writes LDS.
   constexpr int SCI = (3 * HP * C2 + FT - 1) / FT;   // scatter items per thread (<= 5)
   constexpr int A1Q = (2 * XB_AP / 16 + FT - 1) / FT; // a1 16-B pieces per thread (3)
-  const int nsc = npr * HP * C2;
-  // per-thread element offsets of the prefetched inputs (image independent)
-  int goff[SCI], aoffq[A1Q];
-#pragma unroll
-  for (int u = 0; u < SCI; ++u) {
-    const int it = min(tid + u * FT, nsc - 1), pl = it >> 6, co = it & 63;
-    goff[u] = ((pr0 + pl / HP) * HP + pl % HP) * C2 + co;
-  }
+  // per-thread element offsets of the prefetched a1 pieces (unit independent)
+  int aoffq[A1Q];
 #pragma unroll
   for (int u = 0; u < A1Q; ++u) {
     const int i = min(tid + u * FT, 2 * XB_AP / 16 - 1);
     const int pl = i >= XB_AP / 16, k = i - pl * (XB_AP / 16);
     aoffq[u] = pl * A1X_PLANE + 16 * k;
   }
-  const int xoff = d0 * IMG + min(tid, (CB_R + 4) * IMG - 1);
+  const int xoff = min(tid, (CB_R + 4) * IMG - 1);
   uint32_t smk[SCI];
   float sv[SCI], xv = 0.f;
   static_assert(A1Q == 3, "three a1 pieces per thread");
   uint4 a1q0, a1q1, a1q2;             // (named: an array here went to scratch)
-#define X3_PREFETCH(IMG_)                                                                  \
+  // unit geometry: band b covers a1 rows [d0, d0 + aown) and pooled rows [pr0, pr0 + npr)
+#define X3_GEOM(BAND_, D0_, PR0_, NSC_)                                                    \
+  const int D0_ = (BAND_) * CB_R;                                                          \
+  const int PR0_ = (BAND_) == 0 ? 0 : D0_ / 2 - 1;                                         \
+  const int NSC_ = (D0_ / 2 + CB_R / 2 - PR0_) * HP * C2
+#define X3_PREFETCH(UNIT_)                                                                 \
   do {                                                                                     \
-    const int64_t ib_ = (int64_t)(IMG_);                                                   \
+    const int pimg_ = (UNIT_) / CB_S;                                                      \
+    X3_GEOM((UNIT_) - pimg_ * CB_S, pd0_, ppr0_, pnsc_);                                   \
+    const int64_t ib_ = (int64_t)pimg_;                                                    \
     static_for<SCI>([&](auto U) __attribute__((always_inline)) {                          \
       constexpr int u = decltype(U)::value;                                                \
-      smk[u] = pmask[ib_ * FEAT + goff[u]];                                                \
-      sv[u] = dpool[ib_ * FEAT + goff[u]];                                                 \
+      const int go_ = ppr0_ * HP * C2 + min(tid + u * FT, pnsc_ - 1);                      \
+      smk[u] = pmask[ib_ * FEAT + go_];                                                    \
+      sv[u] = dpool[ib_ * FEAT + go_];                                                     \
     });                                                                                    \
-    xv = xng[ib_ * 784 + xoff];                                                            \
-    const char* src_ = a1x + ib_ * 2 * A1X_PLANE + d0 * H1 * 64;                           \
+    xv = xng[ib_ * 784 + pd0_ * IMG + xoff];                                               \
+    const char* src_ = a1x + ib_ * 2 * A1X_PLANE + pd0_ * H1 * 64;                         \
     a1q0 = *reinterpret_cast<const uint4*>(src_ + aoffq[0]);                               \
     a1q1 = *reinterpret_cast<const uint4*>(src_ + aoffq[1]);                               \
     a1q2 = *reinterpret_cast<const uint4*>(src_ + aoffq[2]);                               \
   } while (0)
-  if (grp * ipb < B) X3_PREFETCH(grp * ipb);
+  if (u0 < u1) X3_PREFETCH(u0);
   PDM_STAMP(9);
-  for (int ii = 0; ii < ipb; ++ii) {
-    const int img = grp * ipb + ii;
-    if (img >= B) break;                           // workgroup-uniform
-    __syncthreads();   // the previous image's reads of dz2 / a1 / x are done
+  for (int un = u0; un < u1; ++un) {
+    const int band = un - (un / CB_S) * CB_S;     // workgroup-uniform
+    X3_GEOM(band, d0, pr0, nsc);
+    const int aown = band == CB_S - 1 ? CB_R + 2 : CB_R;
+    const int npx = aown * H1, nmt = (npx + 15) / 16;
+    const bool first = un == u0;
+    __syncthreads();   // the previous unit's reads of dz2 / a1 / x are done
     // ---- staging: zero dz2 (both planes), x rows and a1 plane rows from the registers
 #if !defined(PDM_ABL) || PDM_ABL != 13   // timing ablation only (wrong results)
     for (int i = tid; i < 2 * XB_DP / 16; i += FT)
@@ -1245,7 +1296,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
       }
     }
     __syncthreads();
-    if (ii == 0) PDM_STAMP(10);
+    if (first) PDM_STAMP(10);
     // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
 #if defined(PDM_ABL) && PDM_ABL == 13
     static_for<0>([&](auto U) __attribute__((always_inline)) {
@@ -1269,9 +1320,9 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
         if (py >= d0 / 2) db2p += v;
       }
     });
-    if (ii + 1 < ipb && img + 1 < B) X3_PREFETCH(img + 1);   // lands under this image's compute
+    if (un + 1 < u1) X3_PREFETCH(un + 1);   // lands under this unit's compute
     __syncthreads();
-    if (ii == 0) PDM_STAMP(11);
+    if (first) PDM_STAMP(11);
     // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
 #if defined(PDM_ABL) && PDM_ABL == 11
     for (int mt = wave; mt < 0; mt += 8) {
@@ -1337,7 +1388,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc1[nt] = mfma4(acc[nt][r], xb[r], acc1[nt]);
     }
-    if (ii == 0) PDM_STAMP(12);
+    if (first) PDM_STAMP(12);
     // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
     // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
     // the addresses of pixels col0 + q and col0 + 4 + q of that run, columns 4 pq .. 4 pq + 3
@@ -1386,7 +1437,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
         wacc[j] = mfma3(ah, al, bh, bl, wacc[j]);
       });
     }
-    if (ii == 0) PDM_STAMP(13);
+    if (first) PDM_STAMP(13);
   }
   PDM_STAMP(14);
   __syncthreads();   // dz2 planes free: reduction scratch
@@ -1419,6 +1470,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
 }
 
 #undef X3_PREFETCH
+#undef X3_GEOM
 
 }  // namespace
 
@@ -1477,17 +1529,21 @@ void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float
                                            head_blocks, gwf2, gbf2, gbf1, metrics);
 }
 
-int f32_conv_bwd_blocks(int B, int ipb) { return ((B + ipb - 1) / ipb) * CB_S; }
+// exact: (image group of `per` images) x 6 row bands; split-bf16: `per` (image, band) units
+int f32_conv_bwd_blocks(int B, int per, bool x3) {
+  return x3 ? (B * CB_S + per - 1) / per : ((B + per - 1) / per) * CB_S;
+}
 
 void launch_f32_conv_bwd(const float* a1g, const float* xng, const float* dpool,
                          const uint8_t* pmask, const float* w2, int B, int ipb, float* slab,
                          bool x3, const float* w2x, hipStream_t st) {
+  // ipb: images per workgroup (exact) or (image, band) units per workgroup (split-bf16)
   if (x3) {
-    f32x3_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(
+    f32x3_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb, true), FT, 0, st>>>(
         reinterpret_cast<const char*>(a1g), xng, dpool, pmask, reinterpret_cast<const char*>(w2x),
         B, ipb, slab);
     return;
   }
-  f32_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb), FT, 0, st>>>(a1g, xng, dpool, pmask, w2, B,
-                                                                   ipb, slab);
+  f32_conv_bwd_kernel<<<f32_conv_bwd_blocks(B, ipb, false), FT, 0, st>>>(a1g, xng, dpool, pmask,
+                                                                          w2, B, ipb, slab);
 }

@@ -34,7 +34,8 @@ KNOBS: Dict[str, tuple] = {
     "PDM_FUSE_LIN_REDUCE": ("1", "structure", "0: separate lin_reduce at world size 1 (Linear)"),
     "PDM_LIN_ROWS": (None, "diag", "rows per lin_train workgroup (kernel build constant)"),
     "PDM_F32_CONV": ("x3", "structure", "fp32 CNN conv2 products: x3 (split-bf16) / exact"),
-    "PDM_F32_IPB": (None, "structure", "images per fp32 conv-backward workgroup"),
+    "PDM_F32_IPB": (None, "structure", "images per fp32 (exact) conv-backward workgroup"),
+    "PDM_F32_UPW": (None, "structure", "(image, band) units per split-bf16 conv-backward workgroup"),
     # xGMI transport
     "PDM_XGMI_MODE": ("auto", "structure", "xgmi schedule: auto / one / two"),
     "PDM_XGMI_STREAM": ("1", "structure", "0: per-bucket xgmi launches, no persistent kernel"),

@@ -2,9 +2,8 @@
 
 The reference trains in fp32 (``multi_proc_single_gpu.py:185-191``).  Same chain as the bf16
 program (``cnn_step.py``) with fp32 activations, gradients and weights
-(``csrc/kernels/cnn_f32.hip``).  The conv2 GEMMs run as split-bf16 products on the bf16
-MFMA (``conv_x3``, see below) or exactly on the fp32 MFMA (``v_mfma_f32_16x16x4_f32``);
-fc1 runs on the fp32 MFMA:
+(``csrc/kernels/cnn_f32.hip``).  The conv2 and fc1 GEMMs run as split-bf16 products on the
+bf16 MFMA (``conv_x3``, see below) or exactly on the fp32 MFMA (``v_mfma_f32_16x16x4_f32``):
 
   f32_fwd      gather-free epoch buffer row, normalise, conv1 + ReLU, conv2 + ReLU + maxpool
                -> pool, mask; a1 and the normalised x for the backward
@@ -28,9 +27,17 @@ EVAL_CHUNK = 2048
 SPLITK_TRAIN = 32        # fc1 split-K (divides 288: whole 32-float k chunks per split)
 
 
-def conv_ipb(B: int) -> int:
-    """Images per fp32 conv-backward workgroup (each workgroup stages W2^T once and writes one
-    slab for its images' row band): PDM_F32_IPB overrides."""
+def conv_ipb(B: int, x3: bool = False) -> int:
+    """Work per fp32 conv-backward workgroup (each workgroup stages W2^T once and writes one
+    slab for the work it owns).  Exact kernel: images per workgroup, all of one row band
+    (PDM_F32_IPB overrides).  Split-bf16 kernel: (image, row band) units per workgroup, taken
+    image-major, so that one round of <= 256 workgroups covers the batch (PDM_F32_UPW
+    overrides): half the slabs of 2 rounds of 3-image band groups at the same work per CU."""
+    if x3:
+        env = knobs.get("PDM_F32_UPW")
+        if env:
+            return max(1, int(env))
+        return max(1, -(-B * 6 // 256))
     env = knobs.get("PDM_F32_IPB")
     if env:
         return max(1, int(env))
@@ -71,9 +78,9 @@ class CnnStepF32(GpuStepBase):
         self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=f32,
                                      device=dev)
         self.dpool = torch.empty(B * 9216, dtype=f32, device=dev)
-        self.conv_slab = torch.empty(max(C.f32_conv_bwd_nblk(b, conv_ipb(b))
-                                         for b in range(1, B + 1)) * C.CNN_CONV_SLAB,
-                                     dtype=f32, device=dev)
+        self.conv_slab = torch.empty(max(max(C.f32_conv_bwd_nblk(b, conv_ipb(b, x3), x3)
+                                             for x3 in (False, True)) for b in range(1, B + 1))
+                                     * C.CNN_CONV_SLAB, dtype=f32, device=dev)
         a = self.arena
         self.P = {n: a.param(n) for n in ("conv1.weight", "conv1.bias", "conv2.weight",
                                           "conv2.bias", "fc1.weight", "fc1.bias", "fc2.weight",
@@ -141,10 +148,10 @@ class CnnStepF32(GpuStepBase):
                       self.metrics.train_view(), x3=self.conv_x3)
         red = self.reducer
         red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
-        ipb = conv_ipb(B)
+        ipb = conv_ipb(B, self.conv_x3)
         C.f32_conv_bwd(self.a1g, self.xng, self.dpool, self.pmask, P["conv2.weight"], B,
                        self.conv_slab, ipb, x3=self.conv_x3, w2x=self.w2x)
-        nblk = C.f32_conv_bwd_nblk(B, ipb)
+        nblk = C.f32_conv_bwd_nblk(B, ipb, self.conv_x3)
         if self.fuse_conv_reduce:
             self.launch_optimizer(self._fused_segments(nblk))
             return

@@ -35,13 +35,29 @@ def _reference_net(prog):
     return net
 
 
-def _fp64_grads_with_mask(prog, x, y, pmask, B):
+def _kernel_a1_active(prog, B):
+    """The split-bf16 forward's ReLU decisions for conv1: a1 > 0 iff its hi or lo bf16 part
+    is non-zero, read from the a1 planes it hands the backward (a1g: per image a hi and a lo
+    plane, 26 x 26 pixels x 32 channels, 16-B chunk c of pixel (y, x) at c ^ (x & 3))."""
+    raw = prog.gpu.a1g[:B * 676 * 32].view(torch.int16).view(B, 2, 26, 26, 4, 8).cpu()
+    act = (raw[:, 0] != 0) | (raw[:, 1] != 0)                       # [B, y, x, phys chunk, 8]
+    xi = torch.arange(26).view(1, 1, 26, 1)
+    phys = torch.arange(4).view(1, 1, 1, 4) ^ (xi & 3)              # logical chunk -> physical
+    act = act.gather(3, phys.expand(B, 26, 26, 4).unsqueeze(-1).expand(B, 26, 26, 4, 8))
+    return act.reshape(B, 26, 26, 32).permute(0, 3, 1, 2)
+
+
+def _fp64_grads_with_mask(prog, x, y, pmask, B, a1_active=None):
     """fp64 autograd of the step, max-pool routed by the kernel's own argmax decisions (the
     pool mask): where two window values tie within fp32 rounding, fp32 and fp64 may pick
     different positions, and a gradient routed to a neighbouring pixel is a discrete
-    difference, not a precision one."""
+    difference, not a precision one.  a1_active: conv1's ReLU routed the same way (the
+    split-bf16 conv1 puts a few of the 1.4 M activations per 64 images on the other side of
+    zero; each moves a whole dgrad value into or out of the conv1 gradients)."""
     net = _reference_net(prog).double()
-    a1 = F.relu(net.conv1(x.double()))
+    z1 = net.conv1(x.double())
+    zero = torch.zeros((), dtype=torch.float64)
+    a1 = F.relu(z1) if a1_active is None else torch.where(a1_active, z1, zero)
     z2 = net.conv2(a1)                                            # [B, 64, 24, 24]
     mk = pmask[:B * 9216].view(B, 12, 12, 64).permute(0, 3, 1, 2).cpu().long()
     pos = (mk & 0x80) != 0
@@ -56,13 +72,17 @@ def _fp64_grads_with_mask(prog, x, y, pmask, B):
     return dict(net.named_parameters()), out
 
 
-@pytest.mark.parametrize("conv", ["exact", "x3"])
+@pytest.mark.parametrize("conv,upw", [("exact", None), ("x3", None), ("x3", "4"), ("x3", "7")])
 @pytest.mark.parametrize("B", [64, 37, 256])
-def test_f32_gradients_match_fp32_autograd(gpu, B, conv):
+def test_f32_gradients_match_fp32_autograd(gpu, B, conv, upw, monkeypatch):
     """One training step with lr = 0: the gradient arena holds the step's gradients (the fused
     optimizer writes the reduced conv gradients back).  Compared per parameter with fp64
     autograd of the same step (max-pool routed as the kernel routed it): <= 1e-4 relative,
-    fp32 summation-order noise; and with fp32 autograd (torch's own routing)."""
+    fp32 summation-order noise; and with fp32 autograd (torch's own routing).  upw: (image,
+    band) units per split-bf16 conv-backward workgroup (default: one round of <= 256
+    workgroups), 4 / 7 = workgroups that change image and band mid-way and a partial last one."""
+    if upw is not None:
+        monkeypatch.setenv("PDM_F32_UPW", upw)
     prog, train, _ = _program(B, n=max(2 * B, 300))
     prog.gpu.conv_x3 = conv == "x3"
     idx = distributed_indices(len(train), 1, 0, 0)
@@ -76,7 +96,14 @@ def test_f32_gradients_match_fp32_autograd(gpu, B, conv):
     out = net(x)
     loss = F.cross_entropy(out, train.labels[sel])
     loss.backward()
-    ref64, _ = _fp64_grads_with_mask(prog, x, train.labels[sel], prog.gpu.pmask, B)
+    a1_active = None
+    if conv == "x3":
+        a1_active = _kernel_a1_active(prog, B)
+        with torch.no_grad():
+            z1 = _reference_net(prog).double().conv1(x.double())
+        flips = (a1_active != (z1 > 0)).sum().item()
+        assert flips <= 1e-4 * a1_active.numel(), flips     # rare near-zero activations only
+    ref64, _ = _fp64_grads_with_mask(prog, x, train.labels[sel], prog.gpu.pmask, B, a1_active)
     got = prog.arena.torch_tensors(prog.arena.grads)
     for name, p in net.named_parameters():
         r64 = rel(got[name].double(), ref64[name].grad)
@@ -89,11 +116,16 @@ def test_f32_gradients_match_fp32_autograd(gpu, B, conv):
     assert prog.metrics.buf[1].item() == correct
 
 
-def test_f32_training_tracks_cpu_sgd(gpu):
+@pytest.mark.parametrize("conv,tol", [("exact", 1e-4), ("x3", 5e-4)])
+def test_f32_training_tracks_cpu_sgd(gpu, conv, tol):
     """Several SGD-momentum steps (graph-captured) stay within fp32 noise of the same steps
-    in torch on the CPU, and the evaluation matches."""
+    in torch on the CPU, and the evaluation matches.  Split-bf16 (x3): the conv products'
+    ~1e-5 relative error flips a few ReLU / max-pool decisions that fp32 makes the other way
+    (test_f32_gradients_match_fp32_autograd routes those as the kernel did and holds 1e-4);
+    over 5 steps the parameters drift by up to 1.2e-4 relative, hence 5e-4 here."""
     B = 64
     prog, train, test = _program(B, n=B * 5, lr=0.05, graphs=True, seed=3)
+    prog.gpu.conv_x3 = conv == "x3"
     idx = distributed_indices(len(train), 1, 0, 0)
     net = _reference_net(prog)
     opt = torch.optim.SGD(net.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
@@ -109,13 +141,13 @@ def test_f32_training_tracks_cpu_sgd(gpu):
     got = prog.arena.state_dict()
     for name, p in net.named_parameters():
         r = rel(got["module." + name], p.detach())
-        assert r < 1e-4, (name, r)
+        assert r < tol, (name, r)
     tl, ta = prog.evaluate()
     with torch.no_grad():
         out = net(normalize_reference(test.images).view(-1, 1, 28, 28))
         ref_loss = F.cross_entropy(out, test.labels).item()
         ref_acc = (out.argmax(1) == test.labels).float().mean().item()
-    assert abs(tl.average - ref_loss) < 1e-4 * max(1.0, ref_loss)
+    assert abs(tl.average - ref_loss) < tol * max(1.0, ref_loss)
     assert abs(ta.accuracy - ref_acc) < 1e-6 + 2.0 / len(test.labels)
 
 

@@ -38,3 +38,4 @@ bash tools/pmc_run.sh f32 256 fp32 > $O/pmc_f32.log 2>&1 || exit 1
 bash tools/pmc_run.sh b32force 32 bf16 force > $O/pmc_b32.log 2>&1 || exit 1
 cp gpurun_out/pmc/*.md $O/ && rm -rf gpurun_out/pmc
 echo rc=$?
+# (round-4 final refresh; copy of tools/gpu_refresh.sh)
