@@ -291,29 +291,24 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
   PDM_STAMP(1);
   __syncthreads();   // every wave's staging reads are done: conv1 overwrites the area
   PDM_STAMP(2);
-  // 2. conv1 + bias + ReLU on the bf16 MFMA, split-bf16 with the three partial products packed
-  // into one K = 32 step: slot k = 9 term + tap (k < 27) holds x_hi.w_hi (term 0), x_lo.w_hi
-  // (1), x_hi.w_lo (2) of tap k % 9, slots 27..31 zero; fp32 accumulation from the bias.
-  // A = weights (row = channel 16 nt + i16), B = 16 "virtual pixels" V = 28 y + x of the
-  // 28-wide x image (x = 26, 27 and y >= 26 computed and dropped; x & 3 == lane & 3), so the
-  // lane's D = 4 consecutive channels 16 nt + 4 g .. + 3 of pixel V: one 8-B store per plane
+  // 2. conv1 + bias + ReLU, exact fp32 products on the fp32 MFMA (v_mfma_f32_16x16x4_f32,
+  // taps 4 s + g in k-step s = 0..2, tap 9.. zero; fp32 accumulation from the bias): conv1's
+  // ReLU decisions are the step's first and feed every gradient, so it keeps fp32 products
+  // (split-bf16 here flipped ~15 of 1.4 M activations per 64 images and let a 5-step run drift
+  // 2e-3 from torch fp32).  A = weights (row = channel 16 nt + i16), B = 16 "virtual pixels"
+  // V = 28 y + x of the 28-wide x image (x = 26, 27 and y >= 26 computed and dropped;
+  // x & 3 == lane & 3), so the lane's D = 4 consecutive channels 16 nt + 4 g .. + 3 of pixel V:
+  // one 8-B store per plane.  It was 12.7k cycles as VALU FMAs (4 issue cycles each).
   {
-    bf16x8 wa[2];
-    int xo[8];
-    uint32_t lomask = 0;
+    float wa[2][3];
+    int xo[3];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = 8 * g + e, term = k / 9, tap = k - 9 * term;
-      xo[e] = k < 27 ? (tap / 3) * IMG + tap % 3 : 0;
-      lomask |= (term == 1 ? 1u : 0u) << e;
+    for (int st = 0; st < 3; ++st) {
+      const int tap = 4 * st + g;
+      xo[st] = tap < 9 ? (tap / 3) * IMG + tap % 3 : 0;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const float w = ws[(16 * nt + i16) * 9 + tap];
-        const bf16 whi = to_bf16(w);
-        wa[nt][e] = k >= 27 ? to_bf16(0.f) : term == 2 ? to_bf16(w - from_bf16(whi)) : whi;
-      }
+      for (int nt = 0; nt < 2; ++nt) wa[nt][st] = tap < 9 ? ws[(16 * nt + i16) * 9 + tap] : 0.f;
     }
-    const uint32_t zmask = g == 3 ? 0xF8u : 0u;   // slots 27..31
     f32x4 bias[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -326,20 +321,18 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     for (int tile = wave; tile < (IMG * H1 + 15) / 16; tile += 8) {
 #endif
       const int V = tile * 16 + i16;
-      bf16x8 xb;
+      float xb[3];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = xs[min(V + xo[e], IMG * IMG - 1)];
-        const bf16 h = to_bf16(v);
-        const bf16 l = to_bf16(v - from_bf16(h));
-        xb[e] = (zmask >> e) & 1 ? to_bf16(0.f) : ((lomask >> e) & 1 ? l : h);
-      }
+      for (int st = 0; st < 3; ++st)
+        xb[st] = 4 * st + g < 9 ? xs[min(V + xo[st], IMG * IMG - 1)] : 0.f;
       const int y = V / IMG, x = V - y * IMG;
       const bool ok = y < H1 && x < H1;
       const int ab = (V - 2 * y) * 64 + a1c;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nt], xb, bias[nt], 0, 0, 0);
+        f32x4 acc = bias[nt];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) acc = mfma4(wa[nt][st], xb[st], acc);
         bf16x4 h, l;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

@@ -52,8 +52,9 @@ def _fp64_grads_with_mask(prog, x, y, pmask, B, a1_active=None):
     pool mask): where two window values tie within fp32 rounding, fp32 and fp64 may pick
     different positions, and a gradient routed to a neighbouring pixel is a discrete
     difference, not a precision one.  a1_active: conv1's ReLU routed the same way (the
-    split-bf16 conv1 puts a few of the 1.4 M activations per 64 images on the other side of
-    zero; each moves a whole dgrad value into or out of the conv1 gradients)."""
+    split-bf16 conv2 / fc1 leave conv1's fp32 ReLU decisions alone, so this changes little;
+    a split-bf16 conv1 put ~15 of 1.4 M activations per 64 images on the other side of zero,
+    each moving a whole dgrad value into or out of the conv1 gradients)."""
     net = _reference_net(prog).double()
     z1 = net.conv1(x.double())
     zero = torch.zeros((), dtype=torch.float64)
@@ -116,13 +117,12 @@ def test_f32_gradients_match_fp32_autograd(gpu, B, conv, upw, monkeypatch):
     assert prog.metrics.buf[1].item() == correct
 
 
-@pytest.mark.parametrize("conv,tol", [("exact", 1e-4), ("x3", 5e-4)])
+@pytest.mark.parametrize("conv,tol", [("exact", 1e-4), ("x3", 1e-4)])
 def test_f32_training_tracks_cpu_sgd(gpu, conv, tol):
     """Several SGD-momentum steps (graph-captured) stay within fp32 noise of the same steps
-    in torch on the CPU, and the evaluation matches.  Split-bf16 (x3): the conv products'
-    ~1e-5 relative error flips a few ReLU / max-pool decisions that fp32 makes the other way
-    (test_f32_gradients_match_fp32_autograd routes those as the kernel did and holds 1e-4);
-    over 5 steps the parameters drift by up to 1.2e-4 relative, hence 5e-4 here."""
+    in torch on the CPU, and the evaluation matches, in both product modes.  (A split-bf16
+    conv1 -- measured, not adopted -- flipped a few ReLU decisions per step and drifted
+    2e-3 from torch over these 5 steps; conv1 keeps fp32 products.)"""
     B = 64
     prog, train, test = _program(B, n=B * 5, lr=0.05, graphs=True, seed=3)
     prog.gpu.conv_x3 = conv == "x3"
