@@ -1290,6 +1290,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     }
     __syncthreads();
     if (first) PDM_STAMP(10);
+    if (un == u0 + 1) PDM_STAMP(7);   // the second unit's staging (its inputs prefetched)
     // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
 #if defined(PDM_ABL) && PDM_ABL == 13
     static_for<0>([&](auto U) __attribute__((always_inline)) {

@@ -45,6 +45,8 @@ def show(title, cols, names):
 show("f32x3_fwd", [0, 1, 2, 3, 4, 5, 6],
      ["start", "loads + W2 split + W2T planes", "barrier 1", "conv1 (wave 0)", "barrier 2",
       "conv2 end (wave 0)", "conv2 end (wave 7)"])
+rel7 = (st[:, 7] - st[:, 13]).median().item()
+print(f"f32x3_conv_bwd: second unit staged + barrier, cycles after the first unit's wgrad end: {rel7:.0f}")
 show("f32x3_conv_bwd (first image of blocks 0..255)", [8, 9, 10, 11, 12, 13, 14, 15],
      ["start", "W2T staged + prefetch issued", "staging + barrier", "scatter + barrier",
       "dgrad end (wave 0)", "wgrad end (wave 0)", "all images (wave 0)", "end (slab written)"])
