@@ -1164,7 +1164,7 @@ constexpr int XB_WL = XB_WH + XB_WP;
 constexpr int XB_TOTAL = XB_WL + XB_WP;            // 155136 B
 static_assert(XB_TOTAL <= 163840 && XB_AH % 128 == 0 && XB_DH % 128 == 0 && XB_WH % 128 == 0,
               "f32x3_conv_bwd LDS");
-static_assert((8 * C2 + 8 * 512) * 4 <= 2 * XB_DP, "reduction scratch fits the dz2 planes");
+static_assert((8 * 512 + 8 * FT) * 4 <= 2 * XB_DP, "reduction scratch fits the dz2 planes");
 
 __device__ __forceinline__ int xdz_off(int zp, int chunk) { return zp * 128 + ((chunk ^ (zp & 7)) << 4); }
 __device__ __forceinline__ int xw_off(int tap, int ci, int chunk) {
@@ -1220,12 +1220,12 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
 #pragma unroll
   for (int j = 0; j < 9; ++j) wacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  float db2p = 0.f;
+  float db2p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // channels 8 (tid & 7) + j
   // A unit's global inputs (scatter mask bytes + dpool values, loaded unconditionally from
   // clamped indices; the x rows; the a1 plane rows) are loaded into registers one unit
   // ahead: the next unit's loads are issued after this unit's staging and land while its
   // dgrad / wgrad run, so the staging after the next barrier only writes LDS.
-  constexpr int SCI = (3 * HP * C2 + FT - 1) / FT;   // scatter items per thread (<= 5)
+  static_assert(3 * HP * 8 <= FT, "one whole-window scatter item per thread");
   constexpr int A1Q = (2 * XB_AP / 16 + FT - 1) / FT; // a1 16-B pieces per thread (3)
   // per-thread element offsets of the prefetched a1 pieces (unit independent)
   int aoffq[A1Q];
@@ -1236,8 +1236,9 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     aoffq[u] = pl * A1X_PLANE + 16 * k;
   }
   const int xoff = min(tid, (CB_R + 4) * IMG - 1);
-  uint32_t smk[SCI];
-  float sv[SCI], xv = 0.f;
+  float4 dq0, dq1;                    // the scatter item's 8 pooled gradients
+  uint2 mq;                           // and their 8 pool-mask bytes
+  float xv = 0.f;
   static_assert(A1Q == 3, "three a1 pieces per thread");
   uint4 a1q0, a1q1, a1q2;             // (named: an array here went to scratch)
   // unit geometry: band b covers a1 rows [d0, d0 + aown) and pooled rows [pr0, pr0 + npr)
@@ -1250,18 +1251,20 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     const int pimg_ = (UNIT_) / CB_S;                                                      \
     X3_GEOM((UNIT_) - pimg_ * CB_S, pd0_, ppr0_, pnsc_);                                   \
     const int64_t ib_ = (int64_t)pimg_;                                                    \
-    static_for<SCI>([&](auto U) __attribute__((always_inline)) {                          \
-      constexpr int u = decltype(U)::value;                                                \
-      const int go_ = ppr0_ * HP * C2 + min(tid + u * FT, pnsc_ - 1);                      \
-      smk[u] = pmask[ib_ * FEAT + go_];                                                    \
-      sv[u] = dpool[ib_ * FEAT + go_];                                                     \
-    });                                                                                    \
+    const int64_t eo_ = ib_ * FEAT + ppr0_ * HP * C2 + min(tid, pnsc_ / 8 - 1) * 8;         \
+    dq0 = *reinterpret_cast<const float4*>(dpool + eo_);                                   \
+    dq1 = *reinterpret_cast<const float4*>(dpool + eo_ + 4);                               \
+    mq = *reinterpret_cast<const uint2*>(pmask + eo_);                                     \
     xv = xng[ib_ * 784 + pd0_ * IMG + xoff];                                               \
     const char* src_ = a1x + ib_ * 2 * A1X_PLANE + pd0_ * H1 * 64;                         \
     a1q0 = *reinterpret_cast<const uint4*>(src_ + aoffq[0]);                               \
     a1q1 = *reinterpret_cast<const uint4*>(src_ + aoffq[1]);                               \
     a1q2 = *reinterpret_cast<const uint4*>(src_ + aoffq[2]);                               \
   } while (0)
+  // the dz2 planes zeroed once: the whole-window scatter rewrites every pixel of its rows
+  // (cols 0..23); cols 24, 25, the two pad pixels and local rows 6, 7 are never written
+  for (int i = tid; i < 2 * XB_DP / 16; i += FT)
+    reinterpret_cast<uint4*>(smem + XB_DH)[i] = make_uint4(0u, 0u, 0u, 0u);
   if (u0 < u1) X3_PREFETCH(u0);
   PDM_STAMP(9);
   for (int un = u0; un < u1; ++un) {
@@ -1271,11 +1274,14 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     const int npx = aown * H1, nmt = (npx + 15) / 16;
     const bool first = un == u0;
     __syncthreads();   // the previous unit's reads of dz2 / a1 / x are done
-    // ---- staging: zero dz2 (both planes), x rows and a1 plane rows from the registers
-#if !defined(PDM_ABL) || PDM_ABL != 13   // timing ablation only (wrong results)
-    for (int i = tid; i < 2 * XB_DP / 16; i += FT)
-      reinterpret_cast<uint4*>(smem + XB_DH)[i] = make_uint4(0u, 0u, 0u, 0u);
-#endif
+    // ---- staging: x rows and a1 plane rows from the registers; band 0 re-zeroes local dz2
+    // rows 0, 1 (dz2 rows -2, -1; the previous image's last band wrote real rows there)
+    if (band == 0) {
+      for (int i = tid; i < 2 * 52 * 8; i += FT) {
+        const int pl = i >= 52 * 8, k = i - pl * (52 * 8);
+        reinterpret_cast<uint4*>(smem + XB_DH + pl * XB_DP + 2 * 128)[k] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
     if (tid < (CB_R + 4) * IMG) xs[tid] = xv;
     {
       const uint4 qv[3] = {a1q0, a1q1, a1q2};
@@ -1291,29 +1297,54 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     __syncthreads();
     if (first) PDM_STAMP(10);
     if (un == u0 + 1) PDM_STAMP(7);   // the second unit's staging (its inputs prefetched)
-    // ---- dz2 scatter of pooled rows [pr0, d0 / 2 + 2) (+ db2 of the band's own rows)
-#if defined(PDM_ABL) && PDM_ABL == 13
-    static_for<0>([&](auto U) __attribute__((always_inline)) {
+    // ---- dz2 scatter of pooled rows [pr0, pr0 + npr) (+ db2 of the band's own rows), whole
+    // windows: item (pooled pixel, 8 channels) writes the 16-B chunk of each of its window's
+    // 4 pixels in both planes (the pooled gradient at the channel's argmax if it was
+    // positive, zero elsewhere): 8 ds_write_b128 per item instead of zeroing 60 KB and
+    // 2-byte stores.  Mask byte (f32x3_fwd): 0x80 | 1 << s if the pooled value is > 0, else 0
+#if !defined(PDM_ABL) || PDM_ABL != 13   // timing ablation only (wrong results)
+    if (tid < nsc / 8) {
 #else
-    static_for<SCI>([&](auto U) __attribute__((always_inline)) {
+    if (tid < 0) {
 #endif
-      constexpr int u = decltype(U)::value;
-      const int it = tid + u * FT;
-      const int pl = it >> 6, co = it & 63;
+      const int pl = tid >> 3, c = tid & 7;
       const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
-      const uint32_t mk = smk[u];
-      if (it < nsc && (mk & 0x80)) {
-        const float v = sv[u];
-        const int sidx = __builtin_ctz((unsigned)mk & 0xf);
-        const int lr = 2 * py + (sidx >> 1) - (d0 - 2);
-        const int zp = 2 + lr * H1 + 2 * px + (sidx & 1);
-        const int o = xdz_off(zp, co >> 3) + 2 * (co & 7);
-        const bf16 h = to_bf16(v);
-        *reinterpret_cast<bf16*>(smem + XB_DH + o) = h;
-        *reinterpret_cast<bf16*>(smem + XB_DL + o) = to_bf16(v - from_bf16(h));
-        if (py >= d0 / 2) db2p += v;
+      const float v[8] = {dq0.x, dq0.y, dq0.z, dq0.w, dq1.x, dq1.y, dq1.z, dq1.w};
+      const uint32_t mw[2] = {mq.x, mq.y};
+      uint32_t hp[4], lp[4];             // hi / lo bf16 pairs (channels 2 e, 2 e + 1)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 h0 = to_bf16(v[2 * e]), h1 = to_bf16(v[2 * e + 1]);
+        const bf16 l0 = to_bf16(v[2 * e] - from_bf16(h0)), l1 = to_bf16(v[2 * e + 1] - from_bf16(h1));
+        hp[e] = __builtin_bit_cast(uint16_t, h0) | (uint32_t)__builtin_bit_cast(uint16_t, h1) << 16;
+        lp[e] = __builtin_bit_cast(uint16_t, l0) | (uint32_t)__builtin_bit_cast(uint16_t, l1) << 16;
       }
-    });
+      const bool own = py >= d0 / 2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t m = (mw[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        db2p[j] += own && (m & 0x80u) ? v[j] : 0.f;
+      }
+#pragma unroll
+      for (int sw = 0; sw < 4; ++sw) {
+        const uint32_t need = 0x80u | (1u << sw);
+        uint32_t hq[4], lq[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t m0 = (mw[e >> 1] >> (16 * (e & 1))) & 0xffu;
+          const uint32_t m1 = (mw[e >> 1] >> (16 * (e & 1) + 8)) & 0xffu;
+          const uint32_t keep = ((m0 & need) == need ? 0x0000ffffu : 0u) |
+                                ((m1 & need) == need ? 0xffff0000u : 0u);
+          hq[e] = hp[e] & keep;
+          lq[e] = lp[e] & keep;
+        }
+        const int lr = 2 * py + (sw >> 1) - (d0 - 2);
+        const int zp = 2 + lr * H1 + 2 * px + (sw & 1);
+        const int o = xdz_off(zp, c);
+        *reinterpret_cast<uint4*>(smem + XB_DH + o) = make_uint4(hq[0], hq[1], hq[2], hq[3]);
+        *reinterpret_cast<uint4*>(smem + XB_DL + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+      }
+    }
     if (un + 1 < u1) X3_PREFETCH(un + 1);   // lands under this unit's compute
     __syncthreads();
     if (first) PDM_STAMP(11);
@@ -1447,11 +1478,13 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave * 512 + (nt * 16 + 4 * g + r) * 16 + i16] = acc1[nt][r];
-  red[4096 + tid] = db2p;
+  reinterpret_cast<float4*>(red + 4096)[2 * tid] = make_float4(db2p[0], db2p[1], db2p[2], db2p[3]);
+  reinterpret_cast<float4*>(red + 4096)[2 * tid + 1] = make_float4(db2p[4], db2p[5], db2p[6], db2p[7]);
   __syncthreads();
   if (tid < C2) {
+    // channel tid = 8 c + j: the threads t = c + 8 k held it (fixed order over k)
     float sacc = 0.f;
-    for (int w = 0; w < 8; ++w) sacc += red[4096 + w * 64 + tid];
+    for (int k = 0; k < FT / 8; ++k) sacc += red[4096 + ((tid >> 3) + 8 * k) * 8 + (tid & 7)];
     out[SLB_DB2 + tid] = sacc;
   } else if (tid >= 64 && tid < 64 + C1 * 10) {
     const int e = tid - 64, ci = e / 10, tp = e - 10 * ci;
