@@ -270,6 +270,7 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
     TORCH_CHECK(s.offset % 4 == 0, "segment offsets must be 16-byte aligned");
     s.shadow = nullptr;
     s.shadow_t = nullptr;
+    s.shadow_lo = nullptr;
     s.slab = nullptr;
     s.nslab = 0;
     s.slab_col0 = 0;
@@ -312,9 +313,18 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
       TORCH_CHECK(sh.numel() == (int64_t)s.rows * s.cols, "shadow_t size mismatch");
       s.shadow_t = ptr<__bf16>(sh);
     }
+    if (t.size() > 9 && !t[9].is_none()) {
+      auto sh = t[9].cast<at::Tensor>();
+      need(sh, at::kBFloat16, "shadow_lo");
+      TORCH_CHECK(sh.numel() == (int64_t)s.rows * s.cols, "shadow_lo size mismatch");
+      need_aligned(sh.data_ptr(), 8, "shadow_lo");
+      s.shadow_lo = ptr<__bf16>(sh);
+    }
     s.tonly = (t.size() > 6 && !t[6].is_none() && t[6].cast<bool>()) ? 1 : 0;
     s.tfrag = (t.size() > 7 && !t[7].is_none() && t[7].cast<bool>()) ? 1 : 0;
     s.sfrag = (t.size() > 8 && !t[8].is_none() && t[8].cast<bool>()) ? 1 : 0;
+    TORCH_CHECK(s.shadow_lo == nullptr || (s.shadow != nullptr && s.shadow_t == nullptr && !s.sfrag),
+                "a lo shadow goes with a row-major shadow and no transposed copy");
     if (s.sfrag)
       TORCH_CHECK(s.shadow != nullptr && s.rows % 16 == 0 && s.cols % 32 == 0,
                   "a fragment-major shadow needs a 2-D segment with rows % 16 == 0 and cols % 32 == 0 "
@@ -670,7 +680,7 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
              int64_t B, at::Tensor w1, at::Tensor b1, at::Tensor w2, at::Tensor b2,
              at::Tensor pool, c10::optional<at::Tensor> pmask, c10::optional<at::Tensor> a1g,
              c10::optional<at::Tensor> xng, at::Tensor ylab, int64_t spe, bool x3,
-             c10::optional<at::Tensor> w2x) {
+             c10::optional<at::Tensor> w2x, c10::optional<at::Tensor> w2s) {
   c10::DeviceGuard g(images.device());
   need(images, at::kByte, "images");
   need(labels, at::kInt, "labels");
@@ -689,6 +699,14 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
   need_min(pool, at::kFloat, B * CNN_FEAT, "pool");
   need(ylab, at::kInt, "ylab");
   need_min(ylab, at::kInt, B, "ylab");
+  const __bf16* w2sp = nullptr;
+  if (x3) {
+    TORCH_CHECK(w2s.has_value() && w2s->defined(), "the split-bf16 forward needs w2s");
+    need(*w2s, at::kBFloat16, "w2s");
+    TORCH_CHECK(w2s->numel() == 2 * 64 * 288, "w2s: hi / lo planes of conv2's weight");
+    need_aligned(w2s->data_ptr(), 16, "w2s");
+    w2sp = ptr<__bf16>(*w2s);
+  }
   const bool train = a1g.has_value() && a1g->defined();
   if (train) {
     TORCH_CHECK(pmask.has_value() && xng.has_value(), "training needs pmask, a1g and xng");
@@ -705,7 +723,7 @@ void f32_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> ctr
                  pool.data_ptr<float>(), train ? pmask->data_ptr<uint8_t>() : nullptr,
                  train ? a1g->data_ptr<float>() : nullptr, train ? xng->data_ptr<float>() : nullptr,
                  ylab.data_ptr<int32_t>(), x3,
-                 train && x3 ? w2x_ptr(w2x) : nullptr, cur_stream(images));
+                 train && x3 ? w2x_ptr(w2x) : nullptr, w2sp, cur_stream(images));
 }
 
 void f32_fc1_fwd(at::Tensor pool, at::Tensor w1, at::Tensor part, int64_t B, int64_t splitk,
@@ -845,7 +863,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("f32_fwd", &f32_fwd, py::arg("images"), py::arg("labels"), py::arg("ctr"), py::arg("bfull"),
         py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"), py::arg("pool"),
         py::arg("pmask"), py::arg("a1g"), py::arg("xng"), py::arg("ylab"), py::arg("spe") = 0,
-        py::arg("x3") = false, py::arg("w2x") = py::none());
+        py::arg("x3") = false, py::arg("w2x") = py::none(), py::arg("w2s") = py::none());
   m.def("f32_fc1_fwd", &f32_fc1_fwd, py::arg("pool"), py::arg("w1"), py::arg("part"), py::arg("B"),
         py::arg("splitk"), py::arg("x3") = false);
   m.def("f32_fc1_bwd", &f32_fc1_bwd, py::arg("dh"), py::arg("ldt"), py::arg("pool"), py::arg("w1"),

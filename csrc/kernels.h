@@ -62,6 +62,8 @@ struct OptSeg {
   int32_t first_block; // filled by launch_optim
   __bf16* shadow;      // optional bf16 copy, same layout
   __bf16* shadow_t;    // optional bf16 copy, transposed [cols][rows]
+  __bf16* shadow_lo;   // optional bf16(p - bf16(p)), row-major like shadow: with shadow the
+                       // split-bf16 (hi / lo) operand copy of the fp32 program
   // optional: the gradient is the fixed-order sum of `nslab` per-workgroup slabs
   // (row stride `slab_stride` floats, this segment at column `slab_col0`) — the
   // conv_reduce pass fused into the update (world_size 1: no all-reduce in between)
@@ -220,12 +222,13 @@ void launch_conv_reduce(const float* slab, int nblk, float* gw2, float* gb2, flo
 // ---------------------------------------------------------------- CNN (fp32, cnn_f32.hip)
 // The reference's precision on the fp32 MFMA (v_mfma_f32_16x16x4_f32).  fp32 layouts as the
 // bf16 path (pool [B][12*12][64], pmask, conv2 weight [co][tap][ci], fc1 weight [128][9216]);
+// w2s: conv2's weight as split-bf16 hi / lo planes [2][64][288] (split-bf16 path only).
 // a1g [B][676][32] and xng [B][784] carry the forward's conv1 activations and normalised
 // image to the backward; dh32 [ldt][128] is cnn_head's fp32 dh (launch_cnn_head dh32 != null).
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
                     StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
-                    int32_t* ylab, bool x3, float* w2x, hipStream_t st);
+                    int32_t* ylab, bool x3, float* w2x, const __bf16* w2s, hipStream_t st);
 void launch_f32_fc1_fwd(const float* pool, const float* w1, float* part, int B, int splitk,
                         bool x3, hipStream_t st);
 void launch_f32_fc1_bwd(const float* dh, int ldt, const float* pool, const float* w1, int B,

@@ -208,14 +208,15 @@ constexpr int XF_WS = 3136;                       // fp32 w1 [288] | b1 [32] | b
 constexpr int XF_AH = 4736;                       // bf16 a1 hi plane [676 px][64 B], swizzled
 constexpr int XF_AL = XF_AH + P1 * 64;            // bf16 a1 lo plane
 constexpr int XF_TOTAL = XF_AL + P1 * 64;         // 91264 B
-constexpr int XF_W2R = 292;                       // W2 staging row (floats): 288 + 4 pad
+constexpr int XF_W2RB = 608;                      // W2 hi / lo staging row (bytes): 576 + 32 pad
+constexpr int XF_W2PL = C2 * XF_W2RB;             // one staged plane (38912 B)
 static_assert(XF_TOTAL <= 163840 && XF_AH % 128 == 0 && XF_AL % 128 == 0, "f32x3_fwd LDS");
 
 template <bool TRAIN>
 __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels, int64_t nrow,
     const int64_t* __restrict__ ctr, const StepRows sr, const float* __restrict__ w1,
-    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const float* __restrict__ b1, const bf16* __restrict__ w2s, const float* __restrict__ b2,
     float* __restrict__ pool, uint8_t* __restrict__ pmask, char* __restrict__ a1x,
     float* __restrict__ xng, int32_t* __restrict__ ylab, char* __restrict__ w2x) {
   __shared__ __attribute__((aligned(16))) char smem[XF_TOTAL];
@@ -243,33 +244,33 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     if (TRAIN) reinterpret_cast<float4*>(xng + (int64_t)img * 784)[tid] = x;
   }
   if (tid == 64) ylab[img] = labels[row];
-  // 1. W2 (fp32 [co][tap][ci], 73.7 KB) staged once per workgroup through the a1 planes' LDS
-  // (rows padded to 1168 B): the waves' B fragments were 8 x 36.9 KB of L2 reads per CU,
-  // 75 MB per launch, and the launch's first ~7 us
-  float* w2s = reinterpret_cast<float*>(smem + XF_AH);
-  static_assert(C2 * XF_W2R * 4 <= 2 * P1 * 64, "W2 staging fits the a1 planes");
+  // 1. W2 as split-bf16 hi / lo planes ([co][tap][ci] each; the optimizer writes them with
+  // the fp32 update, CnnStepF32.refresh_shadows after any other change), staged once per
+  // workgroup through the a1 planes' LDS (608-B rows: conflict-free fragment reads): the
+  // waves' own B-fragment loads were 8 x 36.9 KB of L2 reads per CU, 75 MB per launch
+  char* w2st = smem + XF_AH;
+  static_assert(2 * XF_W2PL <= 2 * P1 * 64, "W2 staging fits the a1 planes");
 #pragma unroll
-  for (int u = 0; u < C2 * 288 / 4 / FT; ++u) {
-    const int e = tid + u * FT, co = e / 72, c4 = e - co * 72;
-    reinterpret_cast<float4*>(w2s + co * XF_W2R)[c4] = reinterpret_cast<const float4*>(w2)[e];
+  for (int u = 0; u < 2 * C2 * 576 / 16 / FT; ++u) {
+    const int e = tid + u * FT, pl = e / (C2 * 36), k = e - pl * (C2 * 36);
+    const int r = k / 36, c16 = k - r * 36;
+    *reinterpret_cast<uint4*>(w2st + pl * XF_W2PL + r * XF_W2RB + c16 * 16) =
+        reinterpret_cast<const uint4*>(w2s)[e];
   }
   __syncthreads();
-  // this wave's conv2 B fragments, split: co = 32 nh + 16 j + i16, k = ci = 8 g .. 8 g + 7 of
-  // tap t (W2 internal layout [co][ky][kx][ci])
+  // this wave's conv2 B fragments: co = 32 nh + 16 j + i16, k = ci = 8 g .. 8 g + 7 of tap t
   const int nh = wave & 1;
   bf16x8 bh[9][2], bl[9][2];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const float4* src = reinterpret_cast<const float4*>(w2s + (nh * 32 + j * 16 + i16) * XF_W2R +
-                                                          t * 32 + 8 * g);
-      const float4 p0 = src[0], p1 = src[1];
-      const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-      split8(v, bh[t][j], bl[t][j]);
+      const int o = (nh * 32 + j * 16 + i16) * XF_W2RB + (t * 32 + 8 * g) * 2;
+      bh[t][j] = *reinterpret_cast<const bf16x8*>(w2st + o);
+      bl[t][j] = *reinterpret_cast<const bf16x8*>(w2st + XF_W2PL + o);
     }
-  // pinned here: the compiler would sink the split below conv1 (pressure), where the staging
-  // area is already overwritten
+  // pinned here: the compiler would sink the reads below conv1, where the staging area is
+  // already overwritten
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -278,11 +279,13 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
     // W2^T planes for the backward: chunk (tap, c, ci) = co 8 c .. 8 c + 7 of (tap, ci)
     for (int e = img * FT + tid; e < 9 * 8 * C1; e += gridDim.x * FT) {
       const int ci = e & 31, r = e >> 5, tap = r >> 3, c = r & 7;
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = w2s[(8 * c + u) * XF_W2R + tap * 32 + ci];
       bf16x8 h, l;
-      split8(v, h, l);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = (8 * c + u) * XF_W2RB + (tap * 32 + ci) * 2;
+        h[u] = *reinterpret_cast<const bf16*>(w2st + o);
+        l[u] = *reinterpret_cast<const bf16*>(w2st + XF_W2PL + o);
+      }
       const int o = (tap * C1 + ci) * 128 + ((c ^ (ci & 7)) << 4);
       *reinterpret_cast<bf16x8*>(w2x + o) = h;
       *reinterpret_cast<bf16x8*>(w2x + W2X_PLANE + o) = l;
@@ -1513,15 +1516,15 @@ void read_stamps_f32(unsigned long long* host) {
 void launch_f32_fwd(const uint8_t* images, const int32_t* labels, int64_t nrow, const int64_t* ctr,
                     StepRows sr, int B, const float* w1, const float* b1, const float* w2,
                     const float* b2, float* pool, uint8_t* pmask, float* a1g, float* xng,
-                    int32_t* ylab, bool x3, float* w2x, hipStream_t st) {
+                    int32_t* ylab, bool x3, float* w2x, const __bf16* w2s, hipStream_t st) {
   if (x3) {
     // a1g holds the split a1 planes (same bytes as the fp32 a1), w2x the split W2^T planes
     if (a1g != nullptr)
-      f32x3_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2, pool,
+      f32x3_fwd_kernel<true><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2s, b2, pool,
                                                pmask, reinterpret_cast<char*>(a1g), xng, ylab,
                                                reinterpret_cast<char*>(w2x));
     else
-      f32x3_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2, b2,
+      f32x3_fwd_kernel<false><<<B, FT, 0, st>>>(images, labels, nrow, ctr, sr, w1, b1, w2s, b2,
                                                 pool, pmask, nullptr, xng, ylab, nullptr);
     return;
   }

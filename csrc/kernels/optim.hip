@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       if (KIND == OPT_ADAM) V[e] = v;
       const bf16 hb = to_bf16(p);
       if (s.shadow) s.shadow[shadow_pos(s.sfrag, s.cols, e / s.cols, e % s.cols)] = hb;
+      if (s.shadow_lo) s.shadow_lo[e] = to_bf16(p - from_bf16(hb));
       if (s.shadow_t) s.shadow_t[shadow_t_pos(s.tfrag, s.rows, e / s.cols, e % s.cols)] = hb;
     }
     return;
@@ -174,6 +175,11 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
         if (s.shadow) {
           bf16x4 hb = {to_bf16(p.x), to_bf16(p.y), to_bf16(p.z), to_bf16(p.w)};
           *reinterpret_cast<bf16x4*>(s.shadow + e) = hb;
+          if (s.shadow_lo) {
+            bf16x4 lb = {to_bf16(p.x - from_bf16(hb[0])), to_bf16(p.y - from_bf16(hb[1])),
+                         to_bf16(p.z - from_bf16(hb[2])), to_bf16(p.w - from_bf16(hb[3]))};
+            *reinterpret_cast<bf16x4*>(s.shadow_lo + e) = lb;
+          }
         }
       } else {
         for (int64_t j = e; j < numel && j < e + 4; ++j) {
@@ -183,6 +189,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
           M[j] = m;
           if (KIND == OPT_ADAM) V[j] = v;
           if (s.shadow) s.shadow[j] = to_bf16(p);
+          if (s.shadow_lo) s.shadow_lo[j] = to_bf16(p - from_bf16(to_bf16(p)));
         }
       }
     }

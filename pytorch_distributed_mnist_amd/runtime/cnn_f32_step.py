@@ -68,8 +68,10 @@ class CnnStepF32(GpuStepBase):
         # conv1 activations for the backward: fp32, or (split-bf16 mode) the hi / lo bf16
         # planes in the backward's LDS layout -- the same bytes
         self.a1g = torch.empty(B * 676 * 32, dtype=f32, device=dev)
-        # split-bf16 mode: the W2^T hi / lo planes the forward writes for the backward
+        # split-bf16 mode: the W2^T hi / lo planes the forward writes for the backward, and
+        # conv2's weight as hi / lo planes for the forward (the optimizer keeps them current)
         self.w2x = torch.empty(2 * 9 * 32 * 128 // 4, dtype=f32, device=dev)
+        self.w2split = torch.empty(2 * 64 * 288, dtype=torch.bfloat16, device=dev)
         self.xng = torch.empty(B * 784, dtype=f32, device=dev)
         self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
         part_n = max(SPLITK_TRAIN * B, splitk_eval(EVAL_CHUNK) * EVAL_CHUNK) * 128
@@ -102,13 +104,29 @@ class CnnStepF32(GpuStepBase):
             # hand-off words; the fp32 program uses the transport's per-bucket launches
             self.reducer.streamed = False
         self._fused = {}
+        self.refresh_shadows()
 
+    @torch.no_grad()
     def refresh_shadows(self) -> None:
-        """No bf16 operand copies in the fp32 program."""
+        """Re-derive the split-bf16 copy of conv2's weight (hi = bf16(w), lo = bf16(w - hi))
+        from the fp32 master: the optimizer keeps it current after every update, this covers
+        any other change (construction, a re-broadcast)."""
+        w = self.arena.param("conv2.weight").reshape(-1)
+        n = w.numel()
+        hi = w.to(torch.bfloat16)
+        self.w2split[:n].copy_(hi)
+        self.w2split[n:].copy_((w - hi.float()).to(torch.bfloat16))
+
+    def _seg(self, p, slab=None):
+        """Optimizer segment of parameter p; conv2's weight also writes its hi / lo copy."""
+        off = self.arena.spec.offset(p.name)
+        if p.name == "conv2.weight":
+            n = p.numel
+            return (off, 1, n, self.w2split[:n], None, slab, None, None, None, self.w2split[n:])
+        return (off, 1, p.numel, None, None, slab)
 
     def optimizer_segments(self):
-        spec = self.arena.spec
-        return [(spec.offset(p.name), 1, p.numel, None, None) for p in spec.params]
+        return [self._seg(p) for p in self.arena.spec.params]
 
     def invalidate_graphs(self) -> None:
         super().invalidate_graphs()
@@ -123,11 +141,11 @@ class CnnStepF32(GpuStepBase):
                    "conv1.weight": C.CNN_CONV_SLAB_DW1, "conv1.bias": C.CNN_CONV_SLAB_DB1}
             slab_segs, plain = [], []
             for p in spec.params:
-                sg = (spec.offset(p.name), 1, p.numel, None, None)
                 if p.name in col:
-                    slab_segs.append(sg + ((self.conv_slab, nblk, col[p.name], C.CNN_CONV_SLAB),))
+                    slab_segs.append(self._seg(p, (self.conv_slab, nblk, col[p.name],
+                                                   C.CNN_CONV_SLAB)))
                 else:
-                    plain.append(sg)
+                    plain.append(self._seg(p))
             segs = slab_segs + plain
             self._fused[nblk] = segs
         return segs
@@ -138,7 +156,7 @@ class CnnStepF32(GpuStepBase):
         C.f32_fwd(self.ep_images.view(-1, 784), self.ep_labels, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
                   self.pool, self.pmask, self.a1g, self.xng, self.ylab, spe=self.spe,
-                  x3=self.conv_x3, w2x=self.w2x)
+                  x3=self.conv_x3, w2x=self.w2x, w2s=self.w2split)
         C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, B, SPLITK_TRAIN, x3=self.conv_x3)
         C.cnn_head(self.part, SPLITK_TRAIN, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"],
                    self.ylab, True, None, None, ldt, self.head_slab, self.metrics.train_view(),
@@ -169,7 +187,8 @@ class CnnStepF32(GpuStepBase):
             se = splitk_eval(b)
             C.f32_fwd(self.test_images[s:s + b], self.test_labels[s:s + b], None, b, b,
                       P["conv1.weight"], P["conv1.bias"], P["conv2.weight"], P["conv2.bias"],
-                      self.pool, None, None, None, self.ylab, x3=self.conv_x3)
+                      self.pool, None, None, None, self.ylab, x3=self.conv_x3,
+                      w2s=self.w2split)
             C.f32_fc1_fwd(self.pool, P["fc1.weight"], self.part, b, se, x3=self.conv_x3)
             C.cnn_head(self.part, se, b, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
                        False, None, None, 32, None, self.metrics.eval_view(), None, None)
