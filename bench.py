@@ -419,7 +419,8 @@ def main():
             raise RuntimeError("non-finite parameters after the benchmark")
         ms = elapsed / a.steps * 1e3
         sharded = bool(getattr(prog.gpu, "shard_fc", False))
-        conv2 = ("split-bf16 (hi.hi + hi.lo + lo.hi), fp32 accumulation"
+        conv2 = ("n/a (no convolution)" if model == "linear" else
+                 "split-bf16 (hi.hi + hi.lo + lo.hi), fp32 accumulation"
                  if getattr(prog.gpu, "conv_x3", False) else
                  "fp32 MFMA" if dtype == "fp32" else "bf16 MFMA, fp32 accumulation")
         if shardable:
