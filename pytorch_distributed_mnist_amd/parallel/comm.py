@@ -14,6 +14,7 @@ process group (bench at N=1): every collective is the identity.
 """
 from __future__ import annotations
 
+import atexit
 import itertools
 import time
 
@@ -24,6 +25,33 @@ from ..ops import _ext
 from .dist import default_store, distributed_is_initialized
 
 _uid_counter = itertools.count()
+
+# Native objects (RCCL communicators, gradient reducers, xGMI transports) whose Python owner
+# was garbage-collected without close(): a GC pass can run inside a hipGraph capture, where
+# tearing them down (stream syncs, RCCL finalize, frees) is prohibited and aborts the
+# process, so they are parked here and released at a safe point: release_retired() (the
+# next native construction, the test harness between tests) or interpreter exit.
+_retired: list = []
+
+
+def retire(native) -> None:
+    if native is not None:
+        _retired.append(native)
+
+
+def release_retired() -> None:
+    """Release natives parked by garbage collection (no-op inside a stream capture).
+    Abandoned communicators are aborted: finalize would wait for peers that moved on."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return
+    while _retired:
+        obj = _retired.pop()
+        if hasattr(obj, "abort"):
+            obj.abort()
+        del obj
+
+
+atexit.register(release_retired)
 
 
 class Communicator:
@@ -77,6 +105,7 @@ class RcclComm(Communicator):
     def __init__(self, rank: int, world_size: int, device: torch.device, tag: str | None = None,
                  timeout_s: float = 1800.0):
         C = _ext.require()
+        release_retired()
         self.rank, self.world_size = rank, world_size
         if tag is None:
             tag = str(next(_uid_counter))
@@ -119,6 +148,10 @@ class RcclComm(Communicator):
         if self._c is not None:
             self._c.destroy()
             self._c = None
+
+    def __del__(self):
+        retire(getattr(self, "_c", None))     # never torn down from a GC pass
+        self._c = None
 
 
 def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | None = None,

@@ -37,7 +37,7 @@ from typing import List, Tuple
 import torch
 
 from ..ops import _ext
-from .comm import Communicator, RcclComm, TorchComm
+from .comm import Communicator, RcclComm, TorchComm, release_retired, retire
 from .. import knobs
 
 TRANSPORTS = ("auto", "xgmi", "rccl")
@@ -91,6 +91,7 @@ class GradReducer:
         if isinstance(comm, RcclComm):
             C = _ext.require()
             flat = [b for se in self.bounds for b in se]
+            release_retired()
             self._native = C.GradReducer(comm.handle, grads, flat)
             self.kind = "rccl"
         else:
@@ -224,6 +225,10 @@ class GradReducer:
         if self.kind == "xgmi":
             self._xgmi.close()
 
+    def __del__(self):
+        retire(getattr(self, "_native", None))   # never torn down from a GC pass
+        self._native = None
+
     @property
     def capturable(self) -> bool:
         """True when the whole reduce path can live inside a hipGraph."""
@@ -341,3 +346,7 @@ class XgmiTransport:
         if self.native is not None:
             self.native.close()
             self.native = None
+
+    def __del__(self):
+        retire(getattr(self, "native", None))    # never torn down from a GC pass
+        self.native = None

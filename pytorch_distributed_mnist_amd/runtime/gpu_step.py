@@ -17,6 +17,7 @@ CNN (bf16):  cnn_fwd -> fc1_fwd -> cnn_head -> fc1_bwd -> [all-reduce bucket 0]
 """
 from __future__ import annotations
 
+import gc
 import os
 
 import torch
@@ -231,10 +232,18 @@ class GpuStepBase:
             g = torch.cuda.CUDAGraph()
             saved = self.phase
             self.phase = phase
+            # no garbage collection inside the capture: a GC pass there may tear down native
+            # objects of earlier programs (RCCL finalize, stream syncs, frees), which is
+            # prohibited while capturing and aborts the process (torch.cuda.graph collects
+            # once before the capture begins)
+            gc_on = gc.isenabled()
+            gc.disable()
             try:
                 with torch.cuda.graph(g):          # captured on a side stream
                     self._train_seq(B, nsteps)
             finally:
+                if gc_on:
+                    gc.enable()
                 self.phase = saved              # capturing runs nothing
             self.graphs[key] = g
         return g

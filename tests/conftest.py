@@ -35,3 +35,16 @@ def gpu():
     from pytorch_distributed_mnist_amd.ops import _ext
     _ext.require()          # GPU tests must run the native path: fail loudly if not built
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _release_native_objects():
+    """Between tests: collect the previous test's programs and communicators and release their
+    native parts here, outside any hipGraph capture (parallel/comm.py release_retired)."""
+    yield
+    import sys
+    mod = sys.modules.get("pytorch_distributed_mnist_amd.parallel.comm")
+    if mod is not None:
+        import gc
+        gc.collect()
+        mod.release_retired()
