@@ -42,6 +42,8 @@ def retire(native) -> None:
 def release_retired() -> None:
     """Release natives parked by garbage collection (no-op inside a stream capture).
     Abandoned communicators are aborted: finalize would wait for peers that moved on."""
+    if not _retired:                  # (touches no GPU state: safe in a launcher parent)
+        return
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return
     while _retired:
