@@ -1,0 +1,104 @@
+// Micro-benchmark: cross-workgroup gradient-slab reduction, slab-major vs tile-major layout.
+//
+// The bf16 CNN step's conv backward leaves one fp32 slab (18816 floats) per workgroup and the
+// optimizer sums them (csrc/kernels/optim.hip, slab segments): a workgroup owns 64 elements
+// and reads a 256-B strip from every slab.  This program times that read pattern against a
+// tile-major layout ([tile][slab][64]: one workgroup's reads are one contiguous run), each
+// read right after a writer kernel that produces the slabs (as cnn_bwd does).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o build/slab_layout_bench tools/slab_layout_bench.hip
+//   ./build/slab_layout_bench [nslab] [iters]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); std::exit(1); } } while (0)
+
+constexpr int SLAB = 18816;          // floats per conv slab (dW2 + db2 + dW1 + db1)
+constexpr int NT = SLAB / 64;        // 64-element tiles
+
+__device__ __forceinline__ long addr(bool tiled, int nslab, int w, int e) {
+  return tiled ? ((long)(e / 64) * nslab + w) * 64 + (e % 64) : (long)w * SLAB + e;
+}
+
+__global__ void __launch_bounds__(256) writer(float* s, int nslab, bool tiled, float salt) {
+  const int w = blockIdx.x;
+  for (int e = threadIdx.x; e < SLAB; e += 256) s[addr(tiled, nslab, w, e)] = salt + w + 1e-3f * e;
+}
+
+__global__ void __launch_bounds__(256) reader(const float* s, float* out, int nslab, bool tiled) {
+  __shared__ float4 red[16][16];
+  const int t = blockIdx.x, tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
+  const int e = t * 64 + 4 * c4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j0 = rg; j0 < nslab; j0 += 128) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = min(j0 + 16 * u, nslab - 1);
+      v[u] = *reinterpret_cast<const float4*>(s + addr(tiled, nslab, j, e));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool on = j0 + 16 * u < nslab;
+      acc.x += on ? v[u].x : 0.f;
+      acc.y += on ? v[u].y : 0.f;
+      acc.z += on ? v[u].z : 0.f;
+      acc.w += on ? v[u].w : 0.f;
+    }
+  }
+  red[rg][c4] = acc;
+  __syncthreads();
+  if (tid < 64) {
+    const float* rf = reinterpret_cast<const float*>(&red[0][0]);
+    float g = 0.f;
+    for (int q = 0; q < 16; ++q) g += rf[q * 64 + tid];
+    out[t * 64 + tid] = g;
+  }
+}
+
+int main(int argc, char** argv) {
+  const int nslab = argc > 1 ? std::atoi(argv[1]) : 256;
+  const int iters = argc > 2 ? std::atoi(argv[2]) : 200;
+  float *s, *out;
+  CHECK(hipMalloc(&s, (size_t)nslab * SLAB * sizeof(float)));
+  CHECK(hipMalloc(&out, (size_t)SLAB * sizeof(float)));
+  hipEvent_t ev[3];
+  for (auto& e : ev) CHECK(hipEventCreate(&e));
+  float* host = (float*)std::malloc(SLAB * sizeof(float));
+  for (int tiled = 0; tiled < 2; ++tiled) {
+    double tw = 0, tr = 0;
+    for (int i = 0; i < iters + 10; ++i) {
+      const float salt = (float)(i & 7);
+      CHECK(hipEventRecord(ev[0]));
+      writer<<<nslab, 256>>>(s, nslab, tiled, salt);
+      CHECK(hipEventRecord(ev[1]));
+      reader<<<NT, 256>>>(s, out, nslab, tiled);
+      CHECK(hipEventRecord(ev[2]));
+      CHECK(hipEventSynchronize(ev[2]));
+      float a, b;
+      CHECK(hipEventElapsedTime(&a, ev[0], ev[1]));
+      CHECK(hipEventElapsedTime(&b, ev[1], ev[2]));
+      if (i >= 10) { tw += a; tr += b; }
+    }
+    CHECK(hipMemcpy(host, out, SLAB * sizeof(float), hipMemcpyDeviceToHost));
+    // sum over w of (salt + w + 1e-3 e), salt of the last iteration
+    const float salt = (float)((iters + 9) & 7);
+    double maxerr = 0;
+    for (int e = 0; e < SLAB; ++e) {
+      const double want = (double)nslab * (salt + 1e-3 * e) + 0.5 * nslab * (nslab - 1);
+      const double d = std::abs(host[e] - want) / want;
+      if (d > maxerr) maxerr = d;
+    }
+    const double mb = (double)nslab * SLAB * 4 / 1e6;
+    std::printf("{\"layout\": \"%s\", \"nslab\": %d, \"writer_us\": %.2f, \"reader_us\": %.2f, "
+                "\"reader_GBps\": %.0f, \"max_rel_err\": %.2e}\n",
+                tiled ? "tile-major" : "slab-major", nslab, 1e3 * tw / iters, 1e3 * tr / iters,
+                mb / (tr / iters), maxerr);
+  }
+  std::free(host);
+  CHECK(hipFree(s));
+  CHECK(hipFree(out));
+  return 0;
+}
