@@ -137,8 +137,14 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     load_chunk(0);
     // fused update (fcu.kind >= 0): this tile's fp32 weights and momentum, issued behind the
     // first chunk so they have landed by the epilogue
+    // (with the learning rate and step count: loaded in the epilogue they were one more
+    // memory round trip on its critical path)
     float fpv[DW_MT][4][4], fmv[DW_MT][4][4];
+    double fc_lr = 0.0;
+    int64_t fc_t = 0;
     if (fcu.kind >= 0) {
+      fc_lr = *fcu.lr;
+      fc_t = *fcu.step;
 #pragma unroll
       for (int mt = 0; mt < DW_MT; ++mt)
 #pragma unroll
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       // copy (the transposed copy, which this launch's dX tiles are reading, is re-derived
       // by the optimizer launch).  Same op order as the optimizer kernel: same bits.
       using namespace optim_detail;
-      const Hyper h = make_hyper<OPT_SGD>(fcu);
+      const Hyper h = make_hyper<OPT_SGD>(fcu, fc_lr, fc_t);
       // the bf16 copy is fragment-major (fc1_fwd's B operand, kernels.h frag_pos): this tile
       // is 4 DW_MT n-tiles x 2 k-steps of 1-KB blocks, assembled in LDS and stored as 16-B
       // chunks

@@ -105,15 +105,17 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const float4* sp = reinterpret_cast<const float4*>(s.slab + col);
     const int64_t st4 = s.slab_stride / 4;
     // the update's operands are loaded ahead of the slab reduction (one memory round trip
-    // fewer on the launch's critical path); the hyper-parameters are derived under the loads
+    // fewer on the launch's critical path)
     const int e = e0 + tid;
     const int ec = min(e, (int)numel - 1);
-    float p0 = 0.f, m0 = 0.f, v0 = 0.f;
-    if (tid < 64) {
-      p0 = P[ec];
-      m0 = M[ec];
-      if (KIND == OPT_ADAM) v0 = V[ec];
-    }
+    // unconditional (clamped) loads: loads under `tid < 64` made the compiler wait for them
+    // at the branch join, i.e. before the slab loads below were even issued.  lr and the step
+    // count are loaded here too: loaded by make_hyper after the reduction, they were one more
+    // memory round trip on every workgroup's critical path.
+    const double lr_in = *a.lr;
+    const int64_t t_in = *a.step;
+    const float p0 = P[ec], m0 = M[ec];
+    const float v0 = (KIND == OPT_ADAM) ? V[ec] : 0.f;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int j0 = rg; j0 < s.nslab; j0 += 16 * 8) {
       float4 v[8];
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       }
     }
     red[rg][c4] = acc;
-    const Hyper h = make_hyper<KIND>(a);
+    const Hyper h = make_hyper<KIND>(a, lr_in, t_in);
     __syncthreads();
     if (tid < 64 && e < numel) {
       // a valid element's float4 group is never a clamped one

@@ -12,11 +12,11 @@ struct Hyper {
 };
 
 // A: OptArgs or FcUpdate (the same hyper-parameter field names)
+// lr / t: the device-resident learning rate and step count (*a.lr, *a.step), passed in so a
+// caller can load them early and keep the memory round trip off its critical path
 template <int KIND, class A>
-__device__ __forceinline__ Hyper make_hyper(const A& a) {
+__device__ __forceinline__ Hyper make_hyper(const A& a, double lr, int64_t t) {
   Hyper h;
-  const double lr = *a.lr;
-  const int64_t t = *a.step;
   h.lr = (float)lr;
   h.beta1 = a.beta1; h.beta2 = a.beta2; h.eps = a.eps; h.wd = a.wd;
   h.mom = a.momentum; h.damp = a.dampening; h.nesterov = a.nesterov;
@@ -33,6 +33,11 @@ __device__ __forceinline__ Hyper make_hyper(const A& a) {
     h.bc2_sqrt = 1.f;
   }
   return h;
+}
+
+template <int KIND, class A>
+__device__ __forceinline__ Hyper make_hyper(const A& a) {
+  return make_hyper<KIND>(a, *a.lr, *a.step);
 }
 
 template <int KIND>
