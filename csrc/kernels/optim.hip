@@ -27,19 +27,32 @@ constexpr int TR = 32, TC = 64;
 
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
-  if (a.metrics != nullptr && blockIdx.x == gridDim.x - 1) {
-    pdm_slab_metrics(a.mslab, a.mnslab, a.mcol, a.mstride, a.metrics);
+  // Every workgroup's prologue is a chain of scalar kernel-argument loads: the control
+  // words and every segment's first_block are read up front (one batch, one wait), and the
+  // selected segment is copied whole (a second batch) instead of field by field under the
+  // branches below, each of which waited out its own load.
+  double* const metrics = a.metrics;
+  int64_t* const bump = a.bump;
+  unsigned* const xgp = a.xg;
+  const int nseg = a.nseg;
+  int fb[OPT_MAX_SEG];
+#pragma unroll
+  for (int i = 0; i < OPT_MAX_SEG; ++i) fb[i] = a.seg[i].first_block;
+  int si = 0;
+#pragma unroll
+  for (int i = 1; i < OPT_MAX_SEG; ++i)
+    if (i < nseg && (int)blockIdx.x >= fb[i]) si = i;
+  // pins the search (and the metrics pointer) ahead of the first branch: otherwise the
+  // compiler sinks the first_block loads below the metrics test, a wait apiece
+  asm volatile("" ::"s"(si), "s"(metrics));
+  if (metrics != nullptr && blockIdx.x == gridDim.x - 1) {
+    pdm_slab_metrics(a.mslab, a.mnslab, a.mcol, a.mstride, metrics);
     return;
   }
-  // locate segment
-  int si = 0;
-#pragma unroll 1
-  for (int i = 1; i < a.nseg; ++i)
-    if ((int)blockIdx.x >= a.seg[i].first_block) si = i;
-  const OptSeg& s = a.seg[si];
+  const OptSeg s = a.seg[si];
   const int lb = blockIdx.x - s.first_block;
-  if (a.bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.bump += 1;
-  if (a.xg != nullptr) {
+  if (bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
+  if (xgp != nullptr) {
     // xgmi streamed mode: publish the last bucket (every workgroup stores the same value,
     // so none depends on another being dispatched), then wait for this segment's bucket
     __shared__ int s_go;
