@@ -34,6 +34,8 @@ import time
 
 import torch
 from pytorch_distributed_mnist_amd import knobs
+from pytorch_distributed_mnist_amd.parallel.calibrate import (Candidate, ControlPlane, calibrate,
+                                                              tensor_fingerprint)
 
 # The reference's own training loop with the CNN swapped in, PyTorch eager + DDP/RCCL on one
 # MI355X (tools/reference_eager.py, DataLoader with 4 workers, fp32, SGD momentum, batch 256;
@@ -67,6 +69,30 @@ def parse(argv=None):
                          "group, all-reduces its rank and rank 0 prints one JSON line; tests the "
                          "self-spawn path without a GPU")
     return ap.parse_args(argv)
+
+
+RCCL_MODES = ("carry", "nocarry", "side", "early", "zero")
+
+
+def step_candidates(reducers: dict, model: str, shard_ok) -> list:
+    """Candidate step structures [(name, reducer, structure)]: every transport, and for RCCL
+    the fc-update placement (cnn_step.CnnStep: carry = carried past the next cnn_fwd,
+    nocarry = one grouped launch, side = on a side stream, early = all-reduce issued during
+    the conv backward).  PDM_RCCL_MODE forces one.  'zero' (the fc1 update sharded over the
+    ranks) is a candidate only when forced: its multi-rank RCCL path has not run on hardware
+    yet, so the automatic choice never lands on it."""
+    forced = knobs.get("PDM_RCCL_MODE")
+    if forced is not None and forced not in RCCL_MODES:
+        raise SystemExit(f"PDM_RCCL_MODE={forced!r}: choose from {RCCL_MODES}")
+    cands = []
+    for name, red in reducers.items():
+        if name == "rccl" and model == "cnn":
+            ok = [m for m in RCCL_MODES if m != "zero" or (forced == "zero" and shard_ok(red))]
+            for m in ([forced] if forced in ok else ok):
+                cands.append(("rccl" if m == "carry" else f"rccl-{m}", red, m))
+        else:
+            cands.append((name, red, "carry"))
+    return cands
 
 
 def launch_mode(gpus: int, env) -> str:
@@ -132,22 +158,72 @@ def spawn_ranks(n: int, argv) -> int:
                     p.wait()
 
 
+class _DryStep(Candidate):
+    """A stand-in step structure for --dry-run: a CPU 'replica' advanced deterministically
+    per step, a fixed cost per step, and the fault kinds calibration must survive
+    (PDM_CALIB_FAULT="<rank>:<name>:<phase>": setup / warm / timed / check raise, diverge
+    perturbs this rank's replica, hang stalls the device sync until its deadline)."""
+
+    COST_MS = {"xgmi": 1.0, "rccl": 0.6, "rccl-nocarry": 0.8, "rccl-side": 0.7,
+               "rccl-early": 0.4}
+
+    def __init__(self, name, rank, state, faults):
+        self.name, self.rank, self.state = name, rank, state
+        self.faults = {(int(r), n, p) for r, n, p in
+                       (f.split(":") for f in faults.split(",") if f)} if faults else set()
+
+    def _f(self, phase):
+        return (self.rank, self.name, phase) in self.faults
+
+    def enqueue(self, k):
+        time.sleep(k * self.COST_MS[self.name] * 1e-3)
+        for _ in range(k):
+            self.state.mul_(0.5).add_(1.0)
+        if self._f("diverge"):
+            self.state.add_(1e-3)
+        return k
+
+    def sync(self):
+        if self._f("hang"):
+            time.sleep(0.5)
+            raise RuntimeError(f"calibration ({self.name}) did not finish within 0.5 s")
+
+    def fingerprint(self):
+        return tensor_fingerprint(self.state)
+
+    def recover(self):
+        if torch.distributed.is_initialized():
+            torch.distributed.broadcast(self.state, 0)
+
+
 def dry_run(a, rank: int, ws: int) -> None:
+    """Launch + rendezvous + the calibration protocol on stand-in candidates (gloo, CPU):
+    exercises the self-spawn path and the rank-agreed candidate drop without a GPU."""
     import torch.distributed as dist
     if knobs.get("PDM_BENCH_FAIL_RANK") == str(rank):
         sys.exit(3)                 # fault injection (tests): this rank dies before rendezvous
+    total = 0.0
     if ws > 1:
         dist.init_process_group("gloo", init_method="env://", world_size=ws, rank=rank)
         t = torch.tensor([float(rank)])
         dist.all_reduce(t)
         total = float(t.item())
+    state = torch.zeros(64)
+    faults = knobs.get("PDM_CALIB_FAULT")
+    cands = [_DryStep(n, rank, state, faults) for n in _DryStep.COST_MS]
+    cal = calibrate(cands, ControlPlane(ws), rank, warm_steps=4, timed_steps=16,
+                    inject=faults, log=lambda s: print(f"bench.py: {s}", file=sys.stderr,
+                                                       flush=True))
+    if ws > 1:
         dist.destroy_process_group()
-    else:
-        total = 0.0
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": ws, "rank_sum": total,
                           "launch": "spawned" if knobs.get("PDM_BENCH_SPAWNED") else
-                          ("launcher" if ws > 1 else "single")}), flush=True)
+                          ("launcher" if ws > 1 else "single"),
+                          "config": {"grad_transport": cal.best,
+                                     "transport_calibration_ms_per_step":
+                                         {k: round(v, 4) for k, v in cal.times.items()}},
+                          "comm": {"fallback": cal.notes}}), flush=True)
 
 
 def main():
@@ -226,6 +302,10 @@ def main():
 
     def sync(what):
         parallel.bounded_sync(device, a.timeout, comm, what)
+
+    # a calibration candidate that hangs on the device is cut off sooner than the run's own
+    # deadline (the communicator is then aborted and the run ends with the reason)
+    calib_timeout = min(a.timeout, float(knobs.get("PDM_CALIB_TIMEOUT_S", "60")))
 
     def barrier():
         parallel.control_barrier()      # gloo (CPU tensor): no torch NCCL communicator
@@ -337,63 +417,65 @@ def main():
             if tail:
                 prog.gpu.prepare(tail, sizes=(1,))
 
-        # candidate step structures: every transport, and for RCCL the fc-update placement
-        # (cnn_step.CnnStep: fc_carry = carried past the next cnn_fwd, nocarry = one grouped
-        # launch, fc_side = on a side stream, fc_early = all-reduce issued during the conv
-        # backward, zero = fc1 update sharded over the ranks) unless PDM_RCCL_MODE forces one
-        cands = []
-        forced = knobs.get("PDM_RCCL_MODE")
-        modes = ("carry", "nocarry", "side", "early", "zero")
-        if forced is not None and forced not in modes:
-            raise SystemExit(f"PDM_RCCL_MODE={forced!r}: choose from {modes}")
-        for name, red in reducers.items():
-            if name == "rccl" and model == "cnn":
-                ok = [m for m in modes if m != "zero" or
-                      (shardable and prog.gpu.shard_supported(red))]
-                for m in ([forced] if forced in ok else ok):
-                    cands.append(("rccl" if m == "carry" else f"rccl-{m}", red, m))
-            else:
-                cands.append((name, red, "carry"))
+        cands = step_candidates(reducers, model,
+                                lambda red: shardable and prog.gpu.shard_supported(red))
+
+        def fingerprint():
+            """Bits of this rank's replica (master weights + optimizer state)."""
+            prog.sync_master()
+            sync("fingerprint")
+            return tensor_fingerprint(arena.params, *opt.state_buffers().values())
+
+        def recover():
+            """After a failed candidate: drain, leave sharding, and restore every replica
+            (weights, momentum, bf16 compute copies) from rank 0."""
+            sync("recovery")
+            if shardable:
+                prog.gpu.set_shard_fc(False)
+            for t in (arena.params, *opt.state_buffers().values()):
+                comm.broadcast_(t, 0)
+            if hasattr(prog.gpu, "refresh_shadows"):
+                prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
+            sync("recovery broadcast")
+
+        class Step(Candidate):
+            def __init__(self, name, red, carry):
+                self.name, self.red, self.carry = name, red, carry
+
+            def setup(self):
+                use(self.red, self.carry)
+                prepare()                      # capture outside the calibration window
+
+            def enqueue(self, k):
+                return run(k)
+
+            def sync(self):
+                parallel.bounded_sync(device, calib_timeout, comm, f"calibration ({self.name})")
+
+            def check(self):
+                self.red.check()
+
+            def fingerprint(self):
+                return fingerprint()
+
+            def recover(self):
+                recover()
 
         opt.sync_hyperparams()
         next_epoch()
+        steps = {name: Step(name, red, carry) for name, red, carry in cands}
         calib = {}
         if len(cands) > 1:
-            for name, red, carry in cands:
-                use(red, carry)
-                prepare()                      # capture outside the calibration window
-                run(16)
-                calib[name] = timed(48)[0] / 48 * 1e3
-                try:
-                    red.check()
-                    ok = 1
-                except RuntimeError as e:
-                    print(f"bench.py: {name} transport failed calibration: {e}", file=sys.stderr,
-                          flush=True)
-                    notes.append(f"{name} failed calibration at B={B}: {e}")
-                    ok = 0
-                if ws > 1:                     # every rank drops a transport any rank saw fail
-                    t = torch.tensor([ok], dtype=torch.int32)
-                    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
-                    ok = int(t.item())
-                if not ok:
-                    if name.startswith("rccl"):
-                        raise RuntimeError("rccl transport failed calibration")
-                    del calib[name]
-                    sync("recovery")
-                    if shardable:
-                        prog.gpu.set_shard_fc(False)
-                    # replicas (and their momentum) may differ after a failed reduce
-                    for t in (arena.params, *opt.state_buffers().values()):
-                        comm.broadcast_(t, 0)
-                    if hasattr(prog.gpu, "refresh_shadows"):
-                        prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
-            best = min(calib, key=calib.get)
-            _, red, carry = next(c for c in cands if c[0] == best)
-            use(red, carry)
+            cal = calibrate(list(steps.values()), ControlPlane(ws), rank,
+                            budget_s=float(knobs.get("PDM_CALIB_BUDGET_S", "120")),
+                            inject=knobs.get("PDM_CALIB_FAULT"),
+                            log=lambda s: print(f"bench.py: {s}", file=sys.stderr, flush=True))
+            calib = cal.times
+            notes.extend(f"B={B}: {n}" for n in cal.notes)
+            best = cal.best
         else:
-            use(cands[0][1], cands[0][2])
             best = cands[0][0]
+        use(steps[best].red, steps[best].carry)
         chosen = prog.reducer
         prepare()
         # put the next epoch boundary inside the timed window: continue the current epoch
@@ -417,6 +499,13 @@ def main():
         prog.sync_master()
         if not torch.isfinite(arena.params).all():
             raise RuntimeError("non-finite parameters after the benchmark")
+        if ws > 1:
+            # DDP keeps identical replicas: every rank must hold the same weights and
+            # optimizer state bit for bit after the timed window
+            fps = ControlPlane(ws).allgather_int(fingerprint())
+            if len(set(fps)) != 1:
+                raise RuntimeError(f"replicas diverged during the timed window ({best}): "
+                                   f"fingerprints {fps}")
         ms = elapsed / a.steps * 1e3
         sharded = bool(getattr(prog.gpu, "shard_fc", False))
         conv2 = ("n/a (no convolution)" if model == "linear" else

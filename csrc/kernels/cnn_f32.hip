@@ -1,19 +1,39 @@
 // fp32 CNN step on gfx950: the reference's precision (multi_proc_single_gpu.py trains in fp32,
-// S:185-191) on the fp32 matrix cores, v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32
-// accumulation).  The same chain and fusions as the bf16 kernels, without the bf16 operand
-// copies (the MFMAs read the fp32 master weights directly):
+// S:185-191).  fp32 activations, gradients and master weights throughout; the chain and fusions
+// of the bf16 kernels.  Two sets of kernels:
+//
+// Default (`--dtype fp32`): conv2 and fc1 products as SPLIT-BF16 on the bf16 matrix cores,
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation.  Every fp32 operand is carried as
+// hi = bf16(x), lo = bf16(x - hi), and a product is hi.hi + hi.lo + lo.hi (4.5e-6 relative
+// error per conv output against fp64; TF32 gives 2.9e-4; tests/test_split_bf16.py):
+//
+//   f32x3_fwd      one image / workgroup: normalise -> conv1 + ReLU on the fp32 MFMA
+//                  (16x16x4, exact fp32 products) over the virtual 28-wide pixel grid -> a1
+//                  hi / lo planes in LDS -> conv2 (split-bf16, W2 hi / lo planes written by the
+//                  optimizer and staged once through LDS) with bias + ReLU + 2x2 max-pool in the
+//                  epilogue; training hands a1 and the split W2^T planes to the backward
+//   f32x3_fc1_fwd  split-K GEMM pool . W1^T on split operands -> fp32 partials
+//   f32x3_fc1_bwd  dW1 tiles (K = batch) | dX tiles (K = 128) on split operands | head-slab
+//                  reduction
+//   f32x3_conv_bwd (image, row band) units, one round of <= 256 workgroups, one slab each:
+//                  dz2 scatter, conv2 dgrad fused with relu'(a1) and the conv1 weight/bias
+//                  gradient, conv2 wgrad into persistent accumulators
+//
+// Exact (`PDM_F32_CONV=exact`): every product on the fp32 MFMA, v_mfma_f32_16x16x4_f32:
 //
 //   f32_fwd      one image / workgroup: normalise -> conv1 + ReLU (VALU, exact fp32) into an
 //                LDS a1 image -> conv2 implicit GEMM (M = 576 pixels ordered (pooled pixel,
 //                window position), N = 64, K = 288) with bias + ReLU + 2x2 max-pool fused in
 //                the epilogue -> pooled activations + pool mask; training also writes a1 and
 //                the normalised x for the backward
-//   f32_fc1_fwd  split-K GEMM pool . W1^T -> fp32 partials (the cnn_head kernel sums them,
-//                applies bias + ReLU, fc2, CE and the head backward, writing dh in fp32)
+//   f32_fc1_fwd  split-K GEMM pool . W1^T -> fp32 partials
 //   f32_fc1_bwd  dW1 tiles (K = batch) | dX tiles (K = 128) | head-slab reduction
 //   f32_conv_bwd image row band / workgroup: dz2 = maxpool^-1(dpool) -> conv2 dgrad fused with
 //                relu'(a1) and the conv1 weight/bias gradient, conv2 wgrad -> one fp32 slab per
-//                workgroup (the bf16 kernels' slab layout: conv_reduce / the fused optimizer)
+//                workgroup
+//
+// Both sets share the bf16 program's cnn_head (writing dh in fp32) and the optimizer with the
+// conv slab reduction fused in at world size 1 (the bf16 kernels' slab layout).
 //
 // MFMA 16x16x4 f32 operand layout, lane l = 16 g + i: A[m = i][k = g], B[k = g][n = i],
 // D[m = 4 g + r][n = i] for r = 0..3.

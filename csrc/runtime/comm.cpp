@@ -29,6 +29,7 @@
 #include <rccl/rccl.h>
 #include <torch/extension.h>
 
+#include <atomic>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -73,10 +74,20 @@ py::bytes rccl_unique_id() {
   return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
+// Bring-up cancellation: a communicator init polled in settle() gives up at once when its
+// cancel token is posted here (the Python side posts it from a watcher thread when another
+// rank reports a failed bring-up through the rendezvous store), instead of waiting for
+// peers that will never arrive until the full deadline.
+static std::atomic<int64_t> g_cancelled_init{0};
+
+void rccl_cancel_init(int64_t token) { g_cancelled_init.store(token); }
+
 class RcclComm {
  public:
-  RcclComm(const std::string& uid, int rank, int nranks, int device, double timeout_s)
-      : rank_(rank), nranks_(nranks), device_(device), timeout_s_(timeout_s) {
+  RcclComm(const std::string& uid, int rank, int nranks, int device, double timeout_s,
+           int64_t cancel_token = 0)
+      : rank_(rank), nranks_(nranks), device_(device), timeout_s_(timeout_s),
+        cancel_token_(cancel_token) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad unique id size ", uid.size());
     TORCH_CHECK(timeout_s > 0, "RCCL timeout must be positive");
     ncclUniqueId id;
@@ -91,12 +102,13 @@ class RcclComm {
       TORCH_CHECK(false, "RCCL error ", ncclGetErrorString(r), " at ncclCommInitRankConfig (rank ",
                   rank, " of ", nranks, ")");
     }
-    ncclResult_t st = settle("communicator init");
+    ncclResult_t st = settle("communicator init", /*cancellable=*/true);
     if (st != ncclSuccess) {
       ncclCommAbort(comm_);
       comm_ = nullptr;
       TORCH_CHECK(false, "RCCL communicator init failed on rank ", rank, " of ", nranks, ": ",
-                  st == ncclInProgress ? "timed out after " + std::to_string(timeout_s) +
+                  cancelled_ ? std::string("cancelled: another rank reported a failed bring-up")
+                  : st == ncclInProgress ? "timed out after " + std::to_string(timeout_s) +
                                              " s waiting for the other ranks (a peer never joined "
                                              "or died during bring-up)"
                                        : std::string(ncclGetErrorString(st)));
@@ -112,7 +124,14 @@ class RcclComm {
 
   void destroy() {
     if (comm_) {
-      hipStreamSynchronize(stream_);
+      // the comm stream drains within the deadline, or a collective is stuck on a peer that
+      // never arrives: abort (its kernels exit on RCCL's abort flag) instead of hanging here
+      if (!drain_stream()) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        release_stream();
+        return;
+      }
       // non-blocking communicator: finalize (flushes outstanding operations, in progress
       // until every peer has done the same) is polled against the deadline; a peer that
       // never finalizes gets the communicator aborted instead of a hang in destroy
@@ -140,12 +159,31 @@ class RcclComm {
 
   // Poll the communicator's async state until it leaves ncclInProgress or the deadline
   // passes; returns the final state (ncclInProgress = timed out).
-  ncclResult_t settle(const char* what) {
+  // Poll the comm stream against the deadline (hipStreamQuery, like settle()); false when it
+  // is still busy at the deadline.
+  bool drain_stream() {
+    if (!stream_) return true;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0;; ++i) {
+      hipError_t q = hipStreamQuery(stream_);
+      if (q != hipErrorNotReady) return true;     // done (or an error: nothing left to wait on)
+      const double el =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s_) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(i < 100 ? 10 : 1000));
+    }
+  }
+
+  ncclResult_t settle(const char* what, bool cancellable = false) {
     const auto t0 = std::chrono::steady_clock::now();
     ncclResult_t st = ncclInProgress;
     for (int i = 0;; ++i) {
       if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return ncclInternalError;
       if (st != ncclInProgress) return st;
+      if (cancellable && cancel_token_ != 0 && g_cancelled_init.load() == cancel_token_) {
+        cancelled_ = true;
+        return ncclInProgress;
+      }
       const double el =
           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (el > timeout_s_) return ncclInProgress;
@@ -273,6 +311,8 @@ class RcclComm {
   }
   int rank_, nranks_, device_;
   double timeout_s_;
+  int64_t cancel_token_ = 0;
+  bool cancelled_ = false;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
@@ -409,15 +449,16 @@ class GradReducer {
 
 void register_comm(py::module& m) {
   m.def("rccl_unique_id", &rccl_unique_id, "ncclGetUniqueId() as 128 bytes");
+  m.def("rccl_cancel_init", &rccl_cancel_init, "cancel the RCCL bring-up holding this token");
   m.def("rccl_version", []() {
     int v = 0;
     ncclGetVersion(&v);
     return v;
   });
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init<const std::string&, int, int, int, double>(), py::arg("uid"), py::arg("rank"),
-           py::arg("nranks"), py::arg("device"), py::arg("timeout_s") = 1800.0,
-           py::call_guard<py::gil_scoped_release>())
+      .def(py::init<const std::string&, int, int, int, double, int64_t>(), py::arg("uid"),
+           py::arg("rank"), py::arg("nranks"), py::arg("device"), py::arg("timeout_s") = 1800.0,
+           py::arg("cancel_token") = 0, py::call_guard<py::gil_scoped_release>())
       .def("all_reduce_", &RcclComm::all_reduce_)
       .def("abort", &RcclComm::abort)
       .def("comm_count", &RcclComm::comm_count)

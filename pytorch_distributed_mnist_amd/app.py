@@ -150,11 +150,11 @@ def run(args):
         # collectives it is queued behind), then aborts the communicator and raises
         program.sync_fn = lambda what: parallel.bounded_sync(device, args.timeout, comm, what)
     if getattr(args, "shard_fc", False) and world_size > 1:
-        if program.shard_supported():
+        why = program.shard_unsupported_reason()
+        if why is None:
             program.set_shard_fc(True)
         elif rank == 0:
-            out("warning: --shard-fc needs the CNN over rccl or gloo with a world size that "
-                "splits fc1's 128 rows evenly (16-row shards on the GPU); running unsharded")
+            out("warning: --shard-fc: {}; running unsharded".format(why))
     trainer = Trainer(program)
 
     try:
@@ -179,11 +179,20 @@ def run(args):
                 out('Epoch: {}/{},'.format(epoch, args.epochs),
                     'train loss: {}, train acc: {},'.format(train_loss, train_acc),
                     'test loss: {}, test acc: {}.'.format(test_loss, test_acc))
-                if args.perf and rank == 0:
-                    n = train_loss.count * world_size
-                    out("perf: epoch {} train {:.1f} img/s (node, {} samples in {:.4f}s), "
-                        "eval {:.4f}s".format(epoch, n / max(trainer.last_train_seconds, 1e-12), n,
-                                              trainer.last_train_seconds, trainer.last_eval_seconds))
+                if args.perf:
+                    # node images/sec over the slowest rank's train time (BASELINE.md
+                    # protocol); every rank joins the max (control plane, gloo)
+                    t_train = trainer.last_train_seconds
+                    if world_size > 1 and parallel.distributed_is_initialized():
+                        t = torch.tensor([t_train], dtype=torch.float64)
+                        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+                        t_train = float(t.item())
+                    if rank == 0:
+                        n = train_loss.count * world_size
+                        out("perf: epoch {} train {:.1f} img/s (node, {} samples in {:.4f}s on the "
+                            "slowest rank), eval {:.4f}s".format(
+                                epoch, n / max(t_train, 1e-12), n, t_train,
+                                trainer.last_eval_seconds))
 
                 is_best = test_acc.accuracy > best_acc
                 best_acc = max(test_acc.accuracy, best_acc)

@@ -49,6 +49,11 @@ KNOBS: Dict[str, tuple] = {
     "PDM_BENCH_DEBUG": (None, "diag", "1: print the host timeline of the timed window"),
     "PDM_BENCH_FAIL_RANK": (None, "diag", "fault injection: this rank exits (dry runs)"),
     "PDM_BENCH_SPAWNED": (None, "internal", "set by bench.py on the ranks it starts"),
+    "PDM_CALIB_FAULT": (None, "diag", "fault injection into calibration: "
+                        "<rank>:<candidate>:<setup|warm|timed|check|diverge|hang>[,...]"),
+    "PDM_CALIB_BUDGET_S": ("120", "structure", "wall-clock budget (s) of bench.py's calibration"),
+    "PDM_CALIB_TIMEOUT_S": ("60", "structure", "deadline (s) of one calibration candidate's "
+                            "device sync (the run's --timeout if smaller)"),
     "PDM_GATHER_AHEAD": ("1", "diag", "0: gather each epoch at its boundary"),
     # rehearsal / runtime
     "PDM_SHARE_DEVICE": ("0", "rehearsal", "1: every rank on device 0 (gloo / xgmi tests)"),

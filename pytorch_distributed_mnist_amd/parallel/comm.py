@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import atexit
 import itertools
+import os
+import threading
 import time
 
 import torch
@@ -112,18 +114,45 @@ class RcclComm(Communicator):
         if tag is None:
             tag = str(next(_uid_counter))
         key = f"pdm_amd/rccl_uid/{tag}"
-        if world_size > 1:
-            store = default_store()
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        self.timeout_s = float(timeout_s)
+        if world_size == 1:
+            self._c = C.RcclComm(bytes(C.rccl_unique_id()), rank, 1, dev, float(timeout_s))
+            return
+        # Bring-up with fail-fast: a rank that fails posts `<key>/failed` to the rendezvous
+        # store; peers waiting for the unique id or polling their communicator init (the C++
+        # settle loop, GIL released) see it within ~50 ms and give up, instead of waiting the
+        # whole deadline for a rank that will never arrive.
+        store = default_store()
+        failed = f"{key}/failed"
+        token = int.from_bytes(os.urandom(7), "little") | 1
+        try:
             if rank == 0:
                 uid = C.rccl_unique_id()
                 store.set(key, uid)
             else:
-                uid = store.get(key)
-        else:
-            uid = C.rccl_unique_id()
-        dev = device.index if device.index is not None else torch.cuda.current_device()
-        self._c = C.RcclComm(bytes(uid), rank, world_size, dev, float(timeout_s))
-        self.timeout_s = float(timeout_s)
+                uid = _await_key(store, key, failed, self.timeout_s)
+            stop = threading.Event()
+
+            def watch():
+                while not stop.wait(0.05):
+                    if store.check([failed]):
+                        C.rccl_cancel_init(token)
+                        return
+            w = threading.Thread(target=watch, name="pdm-rccl-init-watch", daemon=True)
+            w.start()
+            try:
+                self._c = C.RcclComm(bytes(uid), rank, world_size, dev, float(timeout_s), token)
+            finally:
+                stop.set()
+                w.join()
+        except Exception as e:
+            try:
+                if not store.check([failed]):
+                    store.set(failed, f"rank {rank}: {e}")
+            except Exception:                  # noqa: BLE001 (the store may be gone too)
+                pass
+            raise
 
     @property
     def handle(self):
@@ -154,6 +183,18 @@ class RcclComm(Communicator):
     def __del__(self):
         retire(getattr(self, "_c", None))     # never torn down from a GC pass
         self._c = None
+
+
+def _await_key(store, key: str, failed: str, timeout_s: float):
+    """store.get(key) that gives up as soon as another rank posts `failed`."""
+    t0 = time.monotonic()
+    while not store.check([key]):
+        if store.check([failed]):
+            raise RuntimeError(f"RCCL bring-up cancelled: {store.get(failed).decode(errors='replace')}")
+        if time.monotonic() - t0 > timeout_s:
+            raise RuntimeError(f"RCCL bring-up: no unique id from rank 0 within {timeout_s:.0f} s")
+        time.sleep(0.01)
+    return store.get(key)
 
 
 def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | None = None,

@@ -21,26 +21,26 @@ import os
 import torch
 
 from .gpu_step import GpuStepBase
-from .. import knobs
+from .structure import StepStructure
 
 EVAL_CHUNK = 2048
 SPLITK_TRAIN = 32        # fc1 split-K (divides 288: whole 32-float k chunks per split)
 
 
-def conv_ipb(B: int, x3: bool = False) -> int:
+def conv_ipb(B: int, x3: bool = False, structure=None) -> int:
     """Work per fp32 conv-backward workgroup (each workgroup stages W2^T once and writes one
     slab for the work it owns).  Exact kernel: images per workgroup, all of one row band
-    (PDM_F32_IPB overrides).  Split-bf16 kernel: (image, row band) units per workgroup, taken
-    image-major, so that one round of <= 256 workgroups covers the batch (PDM_F32_UPW
-    overrides): half the slabs of 2 rounds of 3-image band groups at the same work per CU."""
+    (StepStructure.f32_ipb / PDM_F32_IPB overrides).  Split-bf16 kernel: (image, row band)
+    units per workgroup, taken image-major, so that one round of <= 256 workgroups covers the
+    batch (f32_upw / PDM_F32_UPW overrides): half the slabs of 2 rounds of 3-image band groups
+    at the same work per CU."""
+    st = structure if structure is not None else StepStructure.from_env()
     if x3:
-        env = knobs.get("PDM_F32_UPW")
-        if env:
-            return max(1, int(env))
+        if st.f32_upw:
+            return max(1, int(st.f32_upw))
         return max(1, -(-B * 6 // 256))
-    env = knobs.get("PDM_F32_IPB")
-    if env:
-        return max(1, int(env))
+    if st.f32_ipb:
+        return max(1, int(st.f32_ipb))
     # B = 256, 100-step bench: ipb 1 / 2 / 3 / 6 = 360 / 351 / 340 / 416 us per step
     return max(1, -(-B * 6 // 512))          # <= 2 rounds of 256 workgroups
 
@@ -80,7 +80,8 @@ class CnnStepF32(GpuStepBase):
         self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=f32,
                                      device=dev)
         self.dpool = torch.empty(B * 9216, dtype=f32, device=dev)
-        self.conv_slab = torch.empty(max(max(C.f32_conv_bwd_nblk(b, conv_ipb(b, x3), x3)
+        self.conv_slab = torch.empty(max(max(C.f32_conv_bwd_nblk(b, conv_ipb(b, x3, self.structure),
+                                                                 x3)
                                              for x3 in (False, True)) for b in range(1, B + 1))
                                      * C.CNN_CONV_SLAB, dtype=f32, device=dev)
         a = self.arena
@@ -95,10 +96,7 @@ class CnnStepF32(GpuStepBase):
         # cuDNN's default for fp32 convolutions -- 2.9e-4 (tests/test_split_bf16.py); the
         # step's gradients stay within 1e-4 of fp64 (tests/test_gpu_cnn_f32.py).
         # "exact" = the fp32 MFMA (exact fp32 products, 1.9x the step time).
-        mode = knobs.get("PDM_F32_CONV", "x3")
-        if mode not in ("x3", "exact"):
-            raise ValueError(f"PDM_F32_CONV={mode!r}: x3 or exact")
-        self.conv_x3 = mode == "x3"
+        self.conv_x3 = self.structure.f32_conv == "x3"
         if getattr(self.reducer, "streamed", False):
             # the persistent (streamed) xgmi collective is wired into the bf16 kernels' device
             # hand-off words; the fp32 program uses the transport's per-bucket launches
@@ -166,7 +164,7 @@ class CnnStepF32(GpuStepBase):
                       self.metrics.train_view(), x3=self.conv_x3)
         red = self.reducer
         red.bucket_ready(0)          # fc bucket: travels while the conv backward runs
-        ipb = conv_ipb(B, self.conv_x3)
+        ipb = conv_ipb(B, self.conv_x3, self.structure)
         C.f32_conv_bwd(self.a1g, self.xng, self.dpool, self.pmask, P["conv2.weight"], B,
                        self.conv_slab, ipb, x3=self.conv_x3, w2x=self.w2x)
         nblk = C.f32_conv_bwd_nblk(B, ipb, self.conv_x3)

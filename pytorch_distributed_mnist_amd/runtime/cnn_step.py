@@ -28,7 +28,6 @@ import os
 import torch
 
 from .gpu_step import GpuStepBase
-from .. import knobs
 
 EVAL_CHUNK = 2048
 
@@ -78,12 +77,11 @@ def choose_ipb(B: int, cus: int = 256) -> int:
 BAND_CHOICES = (6, 3, 2)
 
 
-def choose_bands(B: int, cus: int = 256) -> int:
+def choose_bands(B: int, cus: int = 256, forced=None) -> int:
     """Row bands per image in the conv backward: small batches (the reference's per-rank
     split of the node batch, 256 / world_size) spread each image over up to 6 workgroups
     (cnn_bwd_band.hip) so that B * bands fills at most one round of the CUs; 1 = cnn_bwd
-    (PDM_BANDS overrides: 1 disables the split)."""
-    forced = knobs.get("PDM_BANDS")
+    (`forced`, StepStructure.bands / PDM_BANDS, overrides: 1 disables the split)."""
     if forced is not None:
         return int(forced)
     for s in BAND_CHOICES:
@@ -92,19 +90,19 @@ def choose_bands(B: int, cus: int = 256) -> int:
     return 1
 
 
-def choose_fwd_bands(B: int) -> int:
+def choose_fwd_bands(B: int, forced=None, bands_forced=None) -> int:
     """Row bands per image in the forward: the backward's split (the band backward reads the
-    band forward's a1 / normalised x); PDM_FWD_BANDS forces a split of the forward alone (it
-    then hands the one-image backward the uint8 image, as cnn_fwd does)."""
-    forced = knobs.get("PDM_FWD_BANDS")
-    if forced is not None and choose_bands(B) == 1:
+    band forward's a1 / normalised x); `forced` (StepStructure.fwd_bands / PDM_FWD_BANDS)
+    splits the forward alone (it then hands the one-image backward the uint8 image, as
+    cnn_fwd does)."""
+    if forced is not None and choose_bands(B, forced=bands_forced) == 1:
         return int(forced)
-    return choose_bands(B)
+    return choose_bands(B, forced=bands_forced)
 
 
-def conv_blocks(C, B: int) -> int:
+def conv_blocks(C, B: int, bands_forced=None) -> int:
     """Conv-backward workgroups (= gradient slabs) for per-rank batch B."""
-    bands = choose_bands(B)
+    bands = choose_bands(B, forced=bands_forced)
     return C.cnn_bwd_nblk(B, choose_ipb(B) if bands == 1 else 1, bands)
 
 
@@ -113,6 +111,7 @@ class CnnStep(GpuStepBase):
         super().__init__(prog, use_graphs)
         C, dev, B = self.C, self.device, self.bfull
         a = self.arena
+        st = self.structure
         bf16 = torch.bfloat16
         self.ldt = -(-B // 32) * 32
         cap = max(B, EVAL_CHUNK)
@@ -121,7 +120,7 @@ class CnnStep(GpuStepBase):
         self.pmask = torch.empty(cap * 9216, dtype=torch.uint8, device=dev)
         self.xg = torch.empty(B * 784, dtype=torch.uint8, device=dev)
         self.ylab = torch.empty(cap, dtype=torch.int32, device=dev)
-        self.splitk_train = choose_splitk(B, cap=int(knobs.get("PDM_SPLITK_CAP", "32")))
+        self.splitk_train = choose_splitk(B, cap=st.splitk_cap)
         self.splitk_eval = choose_splitk(min(cap, EVAL_CHUNK))
         part_n = max(self.splitk_train * B, self.splitk_eval * EVAL_CHUNK) * 128
         self.part = torch.empty(part_n, dtype=torch.float32, device=dev)
@@ -133,13 +132,13 @@ class CnnStep(GpuStepBase):
         self.ipb = choose_ipb(B)
         # row-band steps (small batches): the forward hands a1 and the normalised x to the
         # backward (cnn_fwd_band -> cnn_bwd_band) instead of the backward recomputing conv1
-        nband = max(b for b in range(1, B + 1) if choose_bands(b) > 1) if \
-            any(choose_bands(b) > 1 for b in range(1, B + 1)) else 0
+        nband = max(b for b in range(1, B + 1) if self.bands(b) > 1) if \
+            any(self.bands(b) > 1 for b in range(1, B + 1)) else 0
         self.a1g = torch.empty(max(nband, 1) * 676 * 32, dtype=bf16, device=dev)
         self.xng = torch.empty(max(nband, 1) * 784, dtype=bf16, device=dev)
         # slabs for every batch size this step runs (the ragged tail may split into more
         # bands than the full batch)
-        self.conv_nblk = max(conv_blocks(C, b) for b in range(1, B + 1))
+        self.conv_nblk = max(conv_blocks(C, b, st.bands) for b in range(1, B + 1))
         self.conv_slab = torch.empty(self.conv_nblk * C.CNN_CONV_SLAB, dtype=torch.float32,
                                      device=dev)
         # bf16 compute copies of the weights (kept current by the optimizer kernel)
@@ -159,22 +158,20 @@ class CnnStep(GpuStepBase):
                                     "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")}
         # world_size 1 (no all-reduce between backward and update): the conv gradient
         # reduction is fused into the optimizer launch (PDM_FUSE_CONV_REDUCE=0 disables)
-        self.fuse_conv_reduce = (not self.reducer.active and
-                                 knobs.get("PDM_FUSE_CONV_REDUCE", "1") != "0")
+        self.fuse_conv_reduce = not self.reducer.active and st.fuse_conv_reduce
         # world_size 1, SGD-momentum: the fc1-weight update runs in fc1_bwd's weight-gradient
         # tiles (the gradient is still in registers; those tiles have slack next to the dX
         # tiles of the same launch); the optimizer launch then only re-derives the transposed
         # bf16 copy W1^T from the updated W1 (PDM_FUSE_FC1=0 disables)
-        self.fuse_fc1 = (self.fuse_conv_reduce and self.opt.kind == "sgd" and
-                         knobs.get("PDM_FUSE_FC1", "1") != "0")
+        self.fuse_fc1 = self.fuse_conv_reduce and self.opt.kind == "sgd" and st.fuse_fc1
         # ... and writes W1^T too, double-buffered by step parity (this step's dX tiles read
         # one half while its weight tiles write the other), so the optimizer launch skips fc1
         # entirely (PDM_FC1_WT2=0: the optimizer re-derives W1^T instead)
-        self.wt_double = knobs.get("PDM_FC1_WT2", "1") != "0"
+        self.wt_double = st.fc1_wt_double
         # the fused fc1 update consumes the fc1-weight gradient in registers; it is stored to
         # the gradient arena only when something will read it (tests comparing gradients set
         # keep_grads; PDM_KEEP_GRADS=1 forces it): 4.7 MB of writes per step otherwise
-        self.keep_grads = knobs.get("PDM_KEEP_GRADS", "0") == "1"
+        self.keep_grads = st.keep_grads
         self.phase_period = 2 if self._wt_double_on() else 1
         self._fused = {}
         # RCCL data plane: where the fc bucket's all-reduce and update go (RCCL_MODES;
@@ -189,7 +186,6 @@ class CnnStep(GpuStepBase):
         #          DDP's Reducer does during loss.backward() (multi_proc_single_gpu.py:91); at
         #          small batches cnn_bwd_band leaves CUs free for RCCL's kernel (B = 32: 192
         #          workgroups on 256 CUs), at B = 256 the collective waits for cnn_bwd
-        self.set_rccl_mode(knobs.get("PDM_RCCL_MODE", "carry"), invalidate=False)
         # world_size > 1: optimizer-state sharding of the fc1 weight (set_shard_fc): its
         # gradient is reduce-scattered instead of all-reduced, each rank updates its
         # 128 / world_size rows (fp32 master, momentum, bf16 W1 rows) and the bf16 W1 rows are
@@ -200,28 +196,52 @@ class CnnStep(GpuStepBase):
         self._shard_rows = None
         self._side = None
         self._side_ev = None
+        self.set_rccl_mode(st.rccl_mode, invalidate=False)
         self.refresh_shadows()
         self._poison_unkept_grads()
 
     RCCL_MODES = ("carry", "nocarry", "side", "early")
 
+    def bands(self, B: int) -> int:
+        """Row bands per image of the conv backward at batch B (choose_bands)."""
+        return choose_bands(B, forced=self.structure.bands)
+
     def set_rccl_mode(self, mode: str, invalidate: bool = True) -> None:
-        """Step structure of the fc bucket on the RCCL data plane (see __init__)."""
-        if mode == "zero":             # bench.py's name for carry + set_shard_fc(True)
+        """Step structure of the fc bucket on the RCCL data plane (see __init__).  'zero' is
+        carry with the fc1 update sharded over the ranks (set_shard_fc); with no reduction
+        (world size 1) the structure is moot and 'zero' runs the local step."""
+        shard = mode == "zero"
+        if shard:
             mode = "carry"
         if mode not in self.RCCL_MODES:
-            raise ValueError(f"RCCL step mode {mode!r}: choose from {self.RCCL_MODES}")
+            raise ValueError(f"RCCL step mode {mode!r}: choose from {self.RCCL_MODES + ('zero',)}")
         self.fc_carry = mode in ("carry", "side")
         self.fc_side = mode == "side"
         self.fc_early = mode == "early"
+        if shard and self.reducer.active:
+            why = self.shard_unsupported_reason()
+            if why is not None:
+                raise ValueError(f"RCCL step mode 'zero' (sharded fc1 update): {why}")
+            self.set_shard_fc(True)
         if invalidate:
             self.invalidate_graphs()
 
     # -- fc1 optimizer-state sharding --------------------------------------------------------
     def shard_supported(self, reducer=None) -> bool:
+        return self.shard_unsupported_reason(reducer) is None
+
+    def shard_unsupported_reason(self, reducer=None):
+        """None when the fc1 update can be sharded over `reducer`'s ranks, else why not."""
         red = reducer or self.reducer
         ws = red.comm.world_size
-        return red.can_shard and 128 % ws == 0 and (128 // ws) % 16 == 0
+        if not red.active:
+            return "no gradient reduction at world size 1"
+        if not red.can_shard:
+            return f"the {red.kind} gradient transport has no reduce-scatter"
+        if 128 % ws or (128 // ws) % 16:
+            return (f"world size {ws} does not split fc1's 128 rows into shards of a multiple "
+                    "of 16 rows")
+        return None
 
     def set_shard_fc(self, on: bool) -> None:
         """Switch the fc1-weight optimizer-state sharding on or off (graphs are re-captured)."""
@@ -349,8 +369,9 @@ class CnnStep(GpuStepBase):
     def fwd_outputs(self, B: int):
         """cnn_fwd's training outputs for per-rank batch B: (xg, ylab, bands, a1g, xng) -- the
         band backward reads a1 + normalised x, the one-image backward the uint8 image."""
-        fb = choose_fwd_bands(B)
-        if choose_bands(B) > 1:
+        st = self.structure
+        fb = choose_fwd_bands(B, st.fwd_bands, st.bands)
+        if self.bands(B) > 1:
             return None, self.ylab, fb, self.a1g, self.xng
         return self.xg, self.ylab, fb, None, None
 
@@ -382,7 +403,7 @@ class CnnStep(GpuStepBase):
         xs = red.sync if red.streamed else None       # xgmi streamed-mode sync words
         ldt = -(-B // 32) * 32
         S = self.splitk_train
-        bands = choose_bands(B)
+        bands = self.bands(B)
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
                   self.pmask, *self.fwd_outputs(B), spe=self.spe)
@@ -405,7 +426,7 @@ class CnnStep(GpuStepBase):
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
         rccl_early = (self.fc_early and not xgmi and red.active and
                       getattr(red, "_native", None) is not None)
-        early = xgmi and not red.streamed and knobs.get("PDM_XGMI_EARLY", "1") != "0"
+        early = xgmi and not red.streamed and self.structure.xgmi_early
         if rccl_early:
             # bucket 0 (fc, 4.7 MB) is complete: its all-reduce goes out now, on the
             # high-priority comm stream, beside the conv backward

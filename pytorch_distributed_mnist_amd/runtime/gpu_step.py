@@ -81,6 +81,7 @@ class GpuStepBase:
         self.use_graphs = bool(use_graphs) and self.reducer.capturable
         self.graphs = {}
         self.bfull = prog.batch_size
+        self.structure = prog.structure
         self.metrics = prog.metrics
         self._opt_segments = None
         # step phase for double-buffered operands (CnnStep's W1^T): a step reads the buffers of
@@ -90,9 +91,6 @@ class GpuStepBase:
         self.phase_period = 1
 
     # -- data ----------------------------------------------------------------
-    # workgroups of the ahead-of-time gather that runs beside the steps (0: one per 16 rows);
-    # grid-striding workgroups take fewer CUs for longer
-    AHEAD_GATHER_WGS = int(knobs.get("PDM_AHEAD_GATHER_WGS", "0"))
 
     def _stage(self, idx: torch.Tensor) -> list:
         """Copy an epoch order into the next pinned staging buffer of a ring of three ([buffer,
@@ -126,7 +124,10 @@ class GpuStepBase:
             self.C.gather_epoch(self.train_images, self.train_labels, buf[0],
                                 self.ep_images.view(-1, 784)[half * n:(half + 1) * n],
                                 self.ep_labels[half * n:(half + 1) * n],
-                                max_wgs=0 if stream is cur_stream else self.AHEAD_GATHER_WGS)
+                                # workgroups of the ahead-of-time gather beside the steps
+                                # (0: one per 16 rows; grid-striding ones take fewer CUs)
+                                max_wgs=0 if stream is cur_stream else
+                                self.structure.ahead_gather_wgs)
             ev = torch.cuda.Event()
             ev.record(stream)
         buf[1] = ev
@@ -331,7 +332,7 @@ class GpuStepBase:
         xg = {}
         if red.streamed:
             waits = red.waits_for(segs)
-            if knobs.get("PDM_XGMI_OPT_WAIT") == "1":
+            if self.structure.xgmi_opt_wait:
                 xg = dict(xg=red.sync, signal_ch=signal_ch, waits=waits, timeout_s=red.timeout_s)
             else:
                 uniq = []
@@ -377,8 +378,7 @@ class LinearStep(GpuStepBase):
         self.gb = self.arena.grad("fc.bias")
         # world size 1 (no all-reduce between backward and update): the slab reduction runs
         # inside the optimizer launch (PDM_FUSE_LIN_REDUCE=0 disables)
-        self.fuse_reduce = (not self.reducer.active and
-                            knobs.get("PDM_FUSE_LIN_REDUCE", "1") != "0")
+        self.fuse_reduce = not self.reducer.active and self.structure.fuse_lin_reduce
         self._fused = {}
 
     def invalidate_graphs(self) -> None:

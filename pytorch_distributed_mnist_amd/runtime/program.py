@@ -23,12 +23,17 @@ import torch
 from ..data.sampler import batch_bounds
 from ..utils.metrics import DeviceMetrics
 from .cpu_step import eval_step_cpu, train_step_cpu
+from .structure import StepStructure
 
 
 class TrainProgram:
     def __init__(self, model: str, dtype: str, arena, optimizer, reducer, train_split, test_split,
-                 batch_size: int, eval_batch: Optional[int] = None, use_graphs: bool = True):
+                 batch_size: int, eval_batch: Optional[int] = None, use_graphs: bool = True,
+                 structure: Optional[StepStructure] = None):
         self.model = model
+        # how the step is laid out (fusions, band splits, collective placement): read from
+        # the PDM_* knobs once, here, unless the caller passes one
+        self.structure = structure if structure is not None else StepStructure.from_env()
         self.dtype = dtype
         self.arena = arena
         self.optimizer = optimizer
@@ -96,12 +101,23 @@ class TrainProgram:
 
     # -- fc1 optimizer-state sharding (CNN, world size > 1) ------------------------------------
     def shard_supported(self) -> bool:
+        return self.shard_unsupported_reason() is None
+
+    def shard_unsupported_reason(self):
+        """None when the fc1 update can be sharded here, else why not (for the user)."""
         if self.model != "cnn":
-            return False
+            return f"the {self.model} model has no fc1 layer to shard"
         if self.gpu is not None:
-            return hasattr(self.gpu, "shard_supported") and self.gpu.shard_supported()
+            if not hasattr(self.gpu, "shard_unsupported_reason"):
+                return (f"the {self.dtype} CNN program has no sharded update "
+                        "(only the bf16 CNN program does)")
+            return self.gpu.shard_unsupported_reason()
         ws = self.reducer.comm.world_size
-        return self.reducer.can_shard and 128 % ws == 0
+        if not self.reducer.can_shard:
+            return f"the {self.reducer.kind} gradient transport has no reduce-scatter"
+        if 128 % ws:
+            return f"world size {ws} does not split fc1's 128 rows evenly"
+        return None
 
     def set_shard_fc(self, on: bool = True) -> None:
         """Shard the fc1 weight's optimizer update over the ranks: its gradient is

@@ -1,0 +1,83 @@
+"""The step structure: every choice of HOW a training step is laid out that does not change
+WHAT it computes (kernel fusions, band splits, split-K, graph length, where the gradient
+buckets' collectives and updates go).
+
+The defaults are the production configuration; ``bench.py`` calibrates the RCCL structure
+on the node.  The ``PDM_*`` structure knobs (knobs.py) are read ONCE, by
+``StepStructure.from_env()``, when a program is built; the step classes only read this
+object, so no production path consults the environment while it builds or captures a step.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, replace
+from typing import Optional
+
+from .. import knobs
+
+RCCL_MODES = ("carry", "nocarry", "side", "early", "zero")
+
+
+@dataclass(frozen=True)
+class StepStructure:
+    # RCCL data plane: placement of the fc bucket's all-reduce and update (cnn_step.CnnStep)
+    rccl_mode: str = "carry"
+    # largest fc1_fwd split-K factor
+    splitk_cap: int = 32
+    # world size 1: the conv slab reduction inside the optimizer launch
+    fuse_conv_reduce: bool = True
+    # world size 1, SGD: fc1's update in fc1_bwd's weight-gradient tiles
+    fuse_fc1: bool = True
+    # ... which also writes W1^T, double-buffered by step parity
+    fc1_wt_double: bool = True
+    # store the fc1 weight gradient the fused update consumes (tests / diagnostics)
+    keep_grads: bool = False
+    # row bands per image of the conv backward / of the forward alone (None = by batch)
+    bands: Optional[int] = None
+    fwd_bands: Optional[int] = None
+    # xgmi: the fc bucket leaves right after fc1_bwd; optimizer workgroups wait per bucket
+    xgmi_early: bool = True
+    xgmi_opt_wait: bool = False
+    # Linear, world size 1: the slab reduction inside the optimizer launch
+    fuse_lin_reduce: bool = True
+    # workgroups of the ahead-of-time epoch gather (0: one per 16 rows)
+    ahead_gather_wgs: int = 0
+    # fp32 CNN: conv2 / fc1 products ("x3" split-bf16, "exact" fp32 MFMA); conv-backward
+    # work per workgroup (None = by batch): (image, band) units (x3) / images (exact)
+    f32_conv: str = "x3"
+    f32_upw: Optional[int] = None
+    f32_ipb: Optional[int] = None
+
+    def __post_init__(self):
+        if self.rccl_mode not in RCCL_MODES:
+            raise ValueError(f"RCCL step mode {self.rccl_mode!r}: choose from {RCCL_MODES}")
+        if self.f32_conv not in ("x3", "exact"):
+            raise ValueError(f"PDM_F32_CONV={self.f32_conv!r}: x3 or exact")
+
+    @classmethod
+    def from_env(cls) -> "StepStructure":
+        """The structure the PDM_* knobs select (unset knobs: the defaults)."""
+        def flag(name, default):
+            v = knobs.get(name)
+            return default if v is None else v != "0"
+
+        def opt_int(name):
+            v = knobs.get(name)
+            return None if v is None else int(v)
+
+        d = cls()
+        return cls(rccl_mode=knobs.get("PDM_RCCL_MODE", d.rccl_mode),
+                   splitk_cap=int(knobs.get("PDM_SPLITK_CAP", str(d.splitk_cap))),
+                   fuse_conv_reduce=flag("PDM_FUSE_CONV_REDUCE", d.fuse_conv_reduce),
+                   fuse_fc1=flag("PDM_FUSE_FC1", d.fuse_fc1),
+                   fc1_wt_double=flag("PDM_FC1_WT2", d.fc1_wt_double),
+                   keep_grads=knobs.get("PDM_KEEP_GRADS", "0") == "1",
+                   bands=opt_int("PDM_BANDS"), fwd_bands=opt_int("PDM_FWD_BANDS"),
+                   xgmi_early=flag("PDM_XGMI_EARLY", d.xgmi_early),
+                   xgmi_opt_wait=knobs.get("PDM_XGMI_OPT_WAIT", "0") == "1",
+                   fuse_lin_reduce=flag("PDM_FUSE_LIN_REDUCE", d.fuse_lin_reduce),
+                   ahead_gather_wgs=int(knobs.get("PDM_AHEAD_GATHER_WGS", "0")),
+                   f32_conv=knobs.get("PDM_F32_CONV", d.f32_conv),
+                   f32_upw=opt_int("PDM_F32_UPW"), f32_ipb=opt_int("PDM_F32_IPB"))
+
+    def with_(self, **kw) -> "StepStructure":
+        return replace(self, **kw)

@@ -69,7 +69,10 @@ def test_spawn_two_ranks_and_world_size_invariance(tmp_path):
     d2.mkdir()
     common = ["--epochs", "1", "--synthetic-size", "2048", "--seed", "11", "--arch", "linear"]
     run_cli(common + ["--world-size", "1"], d1)
-    out = run_cli(common + ["--world-size", "2"], d2)
+    out = run_cli(common + ["--world-size", "2", "--perf"], d2)
+    # --perf: one node img/s line (rank 0) over the slowest rank's train time
+    perf = [l for l in out.splitlines() if l.startswith("perf:")]
+    assert len(perf) == 1 and "on the slowest rank" in perf[0], perf
     assert "rank: 0, device count: 2, workers:2" in out
     assert "rank: 1, device count: 2, workers:2" in out
     ep = [l for l in out.splitlines() if l.startswith("Epoch:")]

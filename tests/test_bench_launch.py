@@ -68,3 +68,59 @@ def test_failing_rank_fails_the_job(tmp_path):
     r = _run(["--gpus", "2", "--dry-run"], env={"PDM_BENCH_FAIL_RANK": "1"})
     assert r.returncode != 0
     assert "rank 1 exited" in r.stderr
+
+
+def _line(r):
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_calibration_without_faults_picks_fastest():
+    d = _line(_run(["--gpus", "2", "--dry-run"]))
+    assert d["config"]["grad_transport"] == "rccl-early"       # the cheapest stand-in
+    assert len(d["config"]["transport_calibration_ms_per_step"]) == 5
+    assert d["comm"]["fallback"] == []
+
+
+def test_calibration_drops_candidates_failing_on_one_rank():
+    """Each kind of failure on ONE rank (an exception in setup / timed steps, a device sync
+    that hits its deadline, replicas that drift apart) drops that candidate on EVERY rank,
+    with the reason recorded; the fastest survivor is chosen and one JSON line printed."""
+    faults = "1:rccl-early:timed,0:rccl:diverge,1:xgmi:hang,0:rccl-side:setup"
+    d = _line(_run(["--gpus", "2", "--dry-run"], env={"PDM_CALIB_FAULT": faults}))
+    assert d["config"]["grad_transport"] == "rccl-nocarry"
+    assert list(d["config"]["transport_calibration_ms_per_step"]) == ["rccl-nocarry"]
+    notes = " | ".join(d["comm"]["fallback"])
+    for what in ("rccl-early failed calibration: timed on rank 1",
+                 "rccl failed calibration: replicas diverged",
+                 "xgmi failed calibration: warm on rank 1",
+                 "rccl-side failed calibration: setup on rank 0"):
+        assert what in notes, notes
+
+
+def test_calibration_failure_in_check_phase_four_ranks():
+    d = _line(_run(["--gpus", "4", "--dry-run"], env={"PDM_CALIB_FAULT": "3:rccl-early:check"}))
+    assert d["config"]["grad_transport"] == "rccl"
+    assert "rccl-early failed calibration: check on rank 3" in d["comm"]["fallback"][0]
+
+
+def test_calibration_with_no_survivor_is_fatal():
+    faults = ",".join(f"1:{n}:setup" for n in ("xgmi", "rccl", "rccl-nocarry", "rccl-side",
+                                                 "rccl-early"))
+    r = _run(["--gpus", "2", "--dry-run"], env={"PDM_CALIB_FAULT": faults})
+    assert r.returncode != 0
+    assert "no step structure survived" in r.stderr
+
+
+def test_zero_is_never_an_automatic_candidate(monkeypatch):
+    b = _bench()
+    reds = {"xgmi": object(), "rccl": object()}
+    monkeypatch.delenv("PDM_RCCL_MODE", raising=False)
+    names = [c[0] for c in b.step_candidates(reds, "cnn", lambda r: True)]
+    assert names == ["xgmi", "rccl", "rccl-nocarry", "rccl-side", "rccl-early"]
+    monkeypatch.setenv("PDM_RCCL_MODE", "zero")
+    assert [c[0] for c in b.step_candidates(reds, "cnn", lambda r: True)] == ["xgmi", "rccl-zero"]
+    monkeypatch.setenv("PDM_RCCL_MODE", "early")
+    assert [c[0] for c in b.step_candidates(reds, "cnn", lambda r: True)] == ["xgmi", "rccl-early"]

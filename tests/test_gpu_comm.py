@@ -146,6 +146,36 @@ def test_rccl_init_times_out_when_a_peer_never_joins(gpu):
     assert time.monotonic() - t0 < 80
 
 
+_CANCELLED = r"""
+import sys, threading, time, torch
+sys.path.insert(0, sys.argv[1])
+from pytorch_distributed_mnist_amd.ops import _ext
+C = _ext.require()
+uid = C.rccl_unique_id()
+threading.Timer(0.5, C.rccl_cancel_init, [4242]).start()   # "another rank failed"
+t0 = time.monotonic()
+try:
+    C.RcclComm(bytes(uid), 0, 2, 0, 60.0, 4242)    # rank 1 never calls init
+except RuntimeError as e:
+    print("RAISED %.2f %s" % (time.monotonic() - t0, e), flush=True)
+    sys.exit(0)
+print("NO ERROR", flush=True)
+sys.exit(1)
+"""
+
+
+def test_rccl_init_cancelled_when_a_peer_reports_failure(gpu):
+    """Fail-fast bring-up: the init's cancel token posted (as parallel.comm's watcher thread
+    does when another rank stores its failure) ends the wait at once, not at the 60 s
+    deadline."""
+    r = subprocess.run([sys.executable, "-c", _CANCELLED, REPO], capture_output=True,
+                       text=True, timeout=90)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RAISED")][0]
+    assert float(line.split()[1]) < 10.0, line
+    assert "cancelled" in line, line
+
+
 def test_bounded_sync_aborts_and_raises(gpu):
     """A device-side wait that outlives the deadline raises from bounded_sync."""
     from pytorch_distributed_mnist_amd.parallel.comm import bounded_sync
