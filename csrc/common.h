@@ -1,6 +1,7 @@
 // Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
 // Wave64 everywhere: lane = threadIdx.x & 63, block sizes are multiples of 64.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -76,17 +77,54 @@ __device__ __forceinline__ float group_sum(float v) {
 __device__ __forceinline__ bf16 to_bf16(float f) { return (bf16)f; }
 __device__ __forceinline__ float from_bf16(bf16 h) { return (float)h; }
 
+// Hand-off stores: bytes a kernel writes for the NEXT launch (gradient slabs, activations,
+// partials, the fused fc1 update).  Plain stores leave them dirty in the writer's XCD L2
+// until the kernel-end release writes them back, which the dependent launch waits for at the
+// boundary (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s).  Agent-scope
+// write-through stores (global_store ... sc1) send them to memory as they are stored,
+// beside the kernel's other work; the readers are other workgroups on other XCDs, so no
+// L2 locality is given up.  PDM_WT selects the site groups (a bitmask, build time):
+//   1 conv gradient slabs (cnn_bwd[_band] -> optimizer / conv_reduce)
+//   2 fc1_bwd outputs (dpool, the fc1 gradient, the fused update's weights and copies)
+//   4 cnn_fwd[_band] outputs (pool, mask, image, a1 / x hand-offs)
+//   8 fc1_fwd split-K partials and cnn_head outputs (dh, dh^T, head slabs)
+#ifndef PDM_WT
+#define PDM_WT 1
+#endif
+template <int G, class T>
+__device__ __forceinline__ void st_ho(T* p, T v) {
+  if constexpr ((PDM_WT & G) == 0) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 16) {
+    unsigned long long w[2];
+    __builtin_memcpy(w, &v, 16);
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    static_assert(sizeof(T) == 1 || sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8,
+                  "hand-off store of 1, 2, 4, 8 or 16 bytes");
+    using U = typename std::conditional<sizeof(T) == 1, unsigned char,
+              typename std::conditional<sizeof(T) == 2, unsigned short,
+              typename std::conditional<sizeof(T) == 4, unsigned int,
+                                        unsigned long long>::type>::type>::type;
+    U u;
+    __builtin_memcpy(&u, &v, sizeof(T));
+    __hip_atomic_store(reinterpret_cast<U*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Stores of per-workgroup gradient slabs (read once, by the next launch).  PDM_NT=1
 // (diagnostic builds): streaming (non-temporal) stores and loads for them.
 #ifndef PDM_NT
 #define PDM_NT 0
 #endif
 __device__ __forceinline__ void pdm_slab_store(float* p, float v) {
-  if (PDM_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  if (PDM_NT == 1) __builtin_nontemporal_store(v, p);
+  else st_ho<1>(p, v);
 }
 __device__ __forceinline__ float4 pdm_slab_load4(const float4* p) {
-  if (PDM_NT) {
+  if (PDM_NT == 1) {
     const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
     return make_float4(v[0], v[1], v[2], v[3]);
   }

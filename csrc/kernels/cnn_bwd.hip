@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         for (int r = 0; r < 4; ++r) {
           const int n = n0 + wave * 16 * DW_MT + mt * 16 + 4 * g + r;
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) gwf1[(int64_t)n * FEAT + k0 + 16 * nt + i16] = acc[mt][nt][r];
+          for (int nt = 0; nt < 4; ++nt) st_ho<2>(&gwf1[(int64_t)n * FEAT + k0 + 16 * nt + i16], acc[mt][nt][r]);
         }
     }
     if (fcu.kind >= 0) {
@@ -227,8 +227,8 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
             const int64_t q = (int64_t)(n0 + nl) * FEAT + k0 + kl;
             float m = fmv[mt][r][nt], v = 0.f;
             const float p = update<OPT_SGD>(fpv[mt][r][nt], acc[mt][nt][r], m, v, h, fcu.grad_scale);
-            fcu.p[q] = p;
-            fcu.m[q] = m;
+            st_ho<2>(&fcu.p[q], p);
+            st_ho<2>(&fcu.m[q], m);
             pt[r] = to_bf16(p);
             fr[(((nl >> 4) * 2 + (kl >> 5)) * 64 + ((kl >> 3) & 3) * 16 + (nl & 15)) * 8 + (kl & 7)] = pt[r];
           }
@@ -241,9 +241,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
       for (int u = 0; u < 2 * DW_MT; ++u) {
         const int c = tid + 256 * u, blk = c >> 6;   // blk = local n-tile * 2 + k-step
-        *reinterpret_cast<uint4*>(fcu.shadow + ((int64_t)((n0 / 16 + (blk >> 1)) * (FEAT / 32) +
-                                                          (k0 >> 5) + (blk & 1)) * 64 + (c & 63)) * 8) =
-            reinterpret_cast<const uint4*>(fr)[c];
+        st_ho<2>(reinterpret_cast<uint4*>(fcu.shadow + ((int64_t)((n0 / 16 + (blk >> 1)) * (FEAT / 32) +
+                                                                   (k0 >> 5) + (blk & 1)) * 64 + (c & 63)) * 8),
+                 reinterpret_cast<const uint4*>(fr)[c]);
       }
       if (fcu.shadow_t_next != nullptr) {
         // local block lb = m-frag * 2 DW_MT + local k-frag -> global block
@@ -253,8 +253,8 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
           const int c = tid + 256 * u, lb = c >> 6;
           const int64_t gb = (int64_t)(k0 / 16 + lb / (2 * DW_MT)) * (HID / 32) + n0 / 32 +
                              lb % (2 * DW_MT);
-          reinterpret_cast<uint4*>(fcu.shadow_t_next)[gb * 64 + (c & 63)] =
-              reinterpret_cast<const uint4*>(frt)[c];
+          st_ho<2>(reinterpret_cast<uint4*>(fcu.shadow_t_next) + gb * 64 + (c & 63),
+                   reinterpret_cast<const uint4*>(frt)[c]);
         }
       }
     }
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
         if (row < B) {
 #pragma unroll
           for (int ft = 0; ft < DX_FT; ++ft)
-            dpool[(int64_t)row * FEAT + f0 + ft * 16 + i16] = to_bf16(acc[ft][bt][r]);
+            st_ho<2>(&dpool[(int64_t)row * FEAT + f0 + ft * 16 + i16], to_bf16(acc[ft][bt][r]));
         }
       }
     FC_STAMP(t, 3);
@@ -948,14 +948,13 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
   if (tid < C2) {
     float s = 0.f;
     for (int w = 0; w < 8; ++w) s += red[RED_DB2 + w * C2 + tid];
-    out[SL_DB2 + tid] = s;
+    pdm_slab_store(&out[SL_DB2 + tid], s);
   } else if (tid >= 64 && tid < 64 + C1 * 10) {
     const int e = tid - 64;             // (ci, tap) with tap 0..8 = weight, 9 = bias
     const int ci = e / 10, t = e - 10 * ci;
     float s = 0.f;
     for (int w = 0; w < 4; ++w) s += red[RED_DW1 + w * C1 * 16 + ci * 16 + t];
-    if (t < 9) out[SL_DW1 + ci * 9 + t] = s;
-    else out[SL_DB1 + ci] = s;
+    pdm_slab_store(t < 9 ? &out[SL_DW1 + ci * 9 + t] : &out[SL_DB1 + ci], s);
   }
 }
 

@@ -417,14 +417,13 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
   if (tid < C2) {
     float s = 0.f;
     for (int w = 0; w < 8; ++w) s += red[RED_DB2 + w * C2 + tid];
-    out[SL_DB2 + tid] = s;
+    pdm_slab_store(&out[SL_DB2 + tid], s);
   } else if (tid >= 64 && tid < 64 + C1 * 10) {
     const int e = tid - 64;
     const int ci = e / 10, t = e - 10 * ci;
     float s = 0.f;
     for (int w = 0; w < 4; ++w) s += red[RED_DW1 + w * C1 * 16 + ci * 16 + t];
-    if (t < 9) out[SL_DW1 + ci * 9 + t] = s;
-    else out[SL_DB1 + ci] = s;
+    pdm_slab_store(t < 9 ? &out[SL_DW1 + ci * 9 + t] : &out[SL_DB1 + ci], s);
   }
   PDM_STAMP(9);
 }

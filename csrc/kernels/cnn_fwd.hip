@@ -139,7 +139,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     // into outputs of the virtual columns 26, 27, which are dropped)
 #pragma unroll
     for (int i = 0; i < 4; ++i) x3[4 * tid + i] = bf16x4{v[i], v[i + 1], v[i + 2], bf16{}};
-    if (TRAIN) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[tid] = xw;
+    if (TRAIN) st_ho<4>(reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784) + tid, xw);
     if (tid == 0) PDM_STAMP_VAL(9, PDM_CLOCK());   // image landed
   }
   __syncthreads();
@@ -272,12 +272,12 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 
   // 4. coalesced write-out of pooled activations + mask
   uint4* pout = reinterpret_cast<uint4*>(pool + (int64_t)img * FEAT);
-  for (int i = tid; i < FEAT * 2 / 16; i += FWD_THREADS) pout[i] = reinterpret_cast<const uint4*>(ps)[i];
+  for (int i = tid; i < FEAT * 2 / 16; i += FWD_THREADS) st_ho<4>(pout + i, reinterpret_cast<const uint4*>(ps)[i]);
   if (TRAIN) {
     uint4* mout = reinterpret_cast<uint4*>(pmask + (int64_t)img * FEAT);
-    for (int i = tid; i < FEAT / 16; i += FWD_THREADS) mout[i] = reinterpret_cast<const uint4*>(ms)[i];
+    for (int i = tid; i < FEAT / 16; i += FWD_THREADS) st_ho<4>(mout + i, reinterpret_cast<const uint4*>(ms)[i]);
   }
-  if (tid == 64) ylab[img] = lab;
+  if (tid == 64) st_ho<4>(ylab + img, lab);
   PDM_STAMP(5);
 }
 
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
       const int row = b0 + 16 * mt + 4 * (lane >> 4) + r;
       if (row < B) {
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) out[(int64_t)row * HID + n0 + 16 * nt + rl] = acc[mt][nt][r];
+        for (int nt = 0; nt < 2; ++nt) st_ho<8>(&out[(int64_t)row * HID + n0 + 16 * nt + rl], acc[mt][nt][r]);
       }
     }
 }
@@ -481,14 +481,14 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
       // row < ldt always: rows >= B write zeros (GEMM padding)
       if (dh32 != nullptr) {
         // fp32 step (cnn_f32.hip): dh row-major in fp32 (rows >= B are zero, GEMM padding)
-        reinterpret_cast<float2*>(dh32 + (int64_t)row * HID)[j] = dhv;
+        st_ho<8>(reinterpret_cast<float2*>(dh32 + (int64_t)row * HID) + j, dhv);
       } else {
         const bf16x2 o = {to_bf16(dhv.x), to_bf16(dhv.y)};
         // both copies fragment-major (kernels.h frag_pos), the layouts fc1_bwd's dW (dh^T: m =
         // hidden unit, k = batch row) and dX (dh: m = batch row, k = hidden unit) tiles load
-        dht[frag_pos(2 * j, row, ldt)] = o[0];
-        dht[frag_pos(2 * j + 1, row, ldt)] = o[1];
-        *reinterpret_cast<bf16x2*>(dh + frag_pos(row, 2 * j, HID)) = o;
+        st_ho<8>(&dht[frag_pos(2 * j, row, ldt)], o[0]);
+        st_ho<8>(&dht[frag_pos(2 * j + 1, row, ldt)], o[1]);
+        st_ho<8>(reinterpret_cast<bf16x2*>(dh + frag_pos(row, 2 * j, HID)), o);
       }
       reinterpret_cast<float2*>(hs[r])[j] = h;
       reinterpret_cast<float2*>(dhs[r])[j] = dhv;
@@ -536,10 +536,10 @@ __global__ __launch_bounds__(256) void cnn_head_kernel(
   }
   float* out = slab + (int64_t)blockIdx.x * HEAD_SLAB;
 #pragma unroll
-  for (int k = 0; k < 5; ++k) out[tid + 256 * k] = sw[k];
-  if (tid < NCLS) out[NCLS * HID + tid] = sx;
-  else if (tid >= 16 && tid < 16 + HID) out[NCLS * HID + NCLS + tid - 16] = sx;
-  else if (tid == 254 || tid == 255) out[HEAD_SLAB - 2 + (tid - 254)] = sx;
+  for (int k = 0; k < 5; ++k) st_ho<8>(&out[tid + 256 * k], sw[k]);
+  if (tid < NCLS) st_ho<8>(&out[NCLS * HID + tid], sx);
+  else if (tid >= 16 && tid < 16 + HID) st_ho<8>(&out[NCLS * HID + NCLS + tid - 16], sx);
+  else if (tid == 254 || tid == 255) st_ho<8>(&out[HEAD_SLAB - 2 + (tid - 254)], sx);
   pdm_bump_counters(c0, c1, c2);
   PDM_STAMP(15);
 }

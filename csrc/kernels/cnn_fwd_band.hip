@@ -129,9 +129,9 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     const int own = band == S - 1 ? XW : R * 7;
     if (TRAIN && tid < own) {
       if (xng != nullptr)
-        reinterpret_cast<bf16x4*>(xng + (int64_t)img * 784)[d0 * 7 + tid] = bf16x4{v[0], v[1], v[2], v[3]};
+        st_ho<4>(reinterpret_cast<bf16x4*>(xng + (int64_t)img * 784) + d0 * 7 + tid, bf16x4{v[0], v[1], v[2], v[3]});
       // the one-image backward (cnn_bwd) reads the gathered uint8 image instead
-      if (xg != nullptr) reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784)[d0 * 7 + tid] = xw;
+      if (xg != nullptr) st_ho<4>(reinterpret_cast<uint32_t*>(xg + (int64_t)img * 784) + d0 * 7 + tid, xw);
     }
   }
   __syncthreads();
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     const int arows = band == S - 1 ? R + 2 : R;
     const uint4* srcv = reinterpret_cast<const uint4*>(a1s);
     uint4* dstv = reinterpret_cast<uint4*>(a1g + (int64_t)img * (P1 * C1) + d0 * H1 * C1);
-    for (int i = tid; i < arows * H1 * 4; i += FTH) dstv[i] = srcv[i];
+    for (int i = tid; i < arows * H1 * 4; i += FTH) st_ho<4>(dstv + i, srcv[i]);
   }
 
   // 3. conv2 implicit GEMM over the band's tiles (local pooled row pyl, px0 % 4 == 0)
@@ -235,12 +235,12 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
   // 4. coalesced write-out of the band's pooled rows + mask
   constexpr int PB = L::RP * HP * C2;            // pooled values per band
   uint4* pout = reinterpret_cast<uint4*>(pool + (int64_t)img * FEAT + p0 * HP * C2);
-  for (int i = tid; i < PB * 2 / 16; i += FTH) pout[i] = reinterpret_cast<const uint4*>(ps)[i];
+  for (int i = tid; i < PB * 2 / 16; i += FTH) st_ho<4>(pout + i, reinterpret_cast<const uint4*>(ps)[i]);
   if (TRAIN) {
     uint4* mout = reinterpret_cast<uint4*>(pmask + (int64_t)img * FEAT + p0 * HP * C2);
-    for (int i = tid; i < PB / 16; i += FTH) mout[i] = reinterpret_cast<const uint4*>(ms)[i];
+    for (int i = tid; i < PB / 16; i += FTH) st_ho<4>(mout + i, reinterpret_cast<const uint4*>(ms)[i]);
   }
-  if (tid == 64 && band == 0) ylab[img] = lab;
+  if (tid == 64 && band == 0) st_ho<4>(ylab + img, lab);
   PDM_STAMP(5);
 }
 

@@ -99,10 +99,19 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
 // BATCH: loads kept in flight per lane before their use (the persistent kernel uses 2 to
 // stay within the 32 registers per lane that cnn_bwd leaves free on a CU).  Indices are
 // 32-bit float4 counts (the host keeps every stage area below 2 GB).
+// PDM_XG_DIAG=1 (diagnostic builds, timing only, wrong results): no payload loads or stores,
+// only the flag protocol, to tell the data movement's cost from the hand-offs'.
+#ifndef PDM_XG_DIAG
+#define PDM_XG_DIAG 0
+#endif
 template <int BATCH>
 __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsigned gen,
                                            long long deadline, int* s_ok) {
   const int tid = threadIdx.x;
+  if (PDM_XG_DIAG == 1) {
+    signal_peers(a, 0, w, gen);
+    return wait_peers(a, 0, w, gen, deadline, s_ok);
+  }
   const int N = a.nranks, r = a.rank;
   const f32x4* src = reinterpret_cast<const f32x4*>(a.src);
   const int n4 = (int)(a.n >> 2);

@@ -67,7 +67,12 @@ constexpr int XG_LOC_READY = XG_LOC_ERR + 8;         // [XG_MAX_CH]
 constexpr int XG_LOC_DONE = XG_LOC_ERR + 16;         // [XG_MAX_CH]
 constexpr int XG_LOC_LSTEP = XG_LOC_ERR + 64;        // [XG_MAX_WG] steps run by the streamed kernel
 constexpr int XG_LOC_WORDS = XG_LOC_LSTEP + XG_MAX_WG;
-constexpr int XG_STREAM_WG = 64;                     // workgroups of the persistent launch
+// workgroups of the persistent launch (PDM_XG_WG: diagnostic builds)
+#ifndef PDM_XG_WG
+#define PDM_XG_WG 64
+#endif
+constexpr int XG_STREAM_WG = PDM_XG_WG;
+static_assert(XG_STREAM_WG >= 1 && XG_STREAM_WG <= XG_MAX_WG, "persistent launch width");
 
 struct XgmiStreamArgs {
   XgmiArgs ch[XG_MAX_CH];

@@ -64,7 +64,10 @@ KNOBS: Dict[str, tuple] = {
     "PDM_STAMPS": (None, "build", "s_memtime phase stamps (diagnostic build)"),
     "PDM_DIAG_ROLES": (None, "build", "fc1_bwd single-role launches"),
     "PDM_NT": (None, "build", "non-temporal slab stores / loads"),
+    "PDM_WT": (None, "build", "write-through hand-off store groups (bitmask, common.h st_ho)"),
     "PDM_ABL": (None, "build", "timing ablations"),
+    "PDM_XG_WG": (None, "build", "workgroups of the persistent xgmi launch (diagnostic builds)"),
+    "PDM_XG_DIAG": (None, "build", "1: xgmi flag protocol without payload (timing only)"),
     "PDM_DG_MTP": (None, "build", "cnn_bwd dgrad tiles per pass"),
     "PDM_DG_PFD": (None, "build", "cnn_bwd dgrad prefetch distance"),
     "PDM_HIPCC_FLAGS": (None, "build", "extra hipcc flags"),

@@ -279,24 +279,35 @@ def test_cnn_trains_and_tracks_cpu(gpu, graphs):
     assert hist[-1][0] < hist[0][0] and hist[-1][2] > 0.8, hist
 
 
-def test_cnn_large_batch_steps(gpu):
+def test_cnn_large_batch_epoch(gpu):
     """BASELINE config 5 shape: batch 8192 per rank (several images per conv-backward
-    workgroup, split-K 1), graph-captured, over an enlarged synthetic set, incl. the ragged
-    tail step of the epoch."""
-    n = 8192 * 2 + 1000
+    workgroup, split-K 1) over an enlarged synthetic set: one whole epoch of 9 full steps
+    (the 8-step graph replayed, then a 1-step graph) and the ragged 1000-image tail, which
+    must give the same bits as the same epoch launched eagerly; a second epoch lowers the
+    loss."""
+    n = 8192 * 9 + 1000
     train = synthetic_split(n, True)
     test = synthetic_split(512, False)
-    p = build_local_program("cnn", "bf16", "cuda", 8192, train, test, optimizer="sgd", lr=0.05,
-                            momentum=0.9, seed=1, use_graphs=True)
-    p.optimizer.sync_hyperparams()
-    p.set_train_indices(distributed_indices(n, 1, 0, 0))
-    tl, ta = p.train_epoch()                 # 2 full steps + a 1000-image tail
-    assert tl.count == n
-    assert torch.isfinite(p.arena.params).all()
-    assert int(p.gpu.ctr[0].item()) == 3
-    p.set_train_indices(distributed_indices(n, 1, 0, 1))
-    tl2, _ = p.train_epoch()
-    assert tl2.count == n and tl2.average < tl.average, (tl.average, tl2.average)
+    res = []
+    for graphs in (True, False):
+        p = build_local_program("cnn", "bf16", "cuda", 8192, train, test, optimizer="sgd",
+                                lr=0.05, momentum=0.9, seed=1, use_graphs=graphs)
+        p.optimizer.sync_hyperparams()
+        p.set_train_indices(distributed_indices(n, 1, 0, 0))
+        tl, ta = p.train_epoch()                 # 9 full steps + the 1000-image tail
+        assert tl.count == n
+        assert torch.isfinite(p.arena.params).all()
+        assert int(p.gpu.ctr[0].item()) == 10
+        torch.cuda.synchronize()
+        res.append((p.arena.params.clone(), p.optimizer.momentum_buffer.clone(), tl.average))
+        if graphs:
+            assert (8192, 8, 0) in p.gpu.graphs or any(k[:2] == (8192, 8) for k in p.gpu.graphs)
+            keep = p
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert res[0][2] == res[1][2]
+    keep.set_train_indices(distributed_indices(n, 1, 0, 1))
+    tl2, _ = keep.train_epoch()
+    assert tl2.count == n and tl2.average < res[0][2], (res[0][2], tl2.average)
 
 
 def test_fused_conv_reduce_matches_separate_pass(gpu):
