@@ -260,6 +260,13 @@ def main():
     # PDM_FORCE_COMM=1 at N=1: run the multi-GPU step structure (conv reduction, bucket
     # all-reduces through a 1-rank communicator) to price it without transfers
     force_comm = knobs.get("PDM_FORCE_COMM") == "1"
+    # PDM_EMULATE_WS=N with PDM_FORCE_COMM=1 and PDM_RCCL_MODE=zero: the per-rank chain of an
+    # N-rank job (the fc1 update sharded over 128 / N rows, collectives of the 1-rank
+    # communicator) priced on one GPU; reported under config.emulated_world_size
+    emulate = knobs.get("PDM_EMULATE_WS")
+    if emulate is not None and not (force_comm and ws == 1):
+        raise SystemExit("PDM_EMULATE_WS prices one rank's chain on one GPU: it needs "
+                         "PDM_FORCE_COMM=1 and --gpus 1")
     model = a.model
     spec = get_spec(model)
     parallel.verify_params_across_ranks(spec, rank, ws)
@@ -574,6 +581,8 @@ def main():
             "launch": "spawned" if knobs.get("PDM_BENCH_SPAWNED") else
                       ("launcher" if ws > 1 else "single"),
         }
+        if emulate is not None:
+            line["config"]["emulated_world_size"] = int(emulate)
         if main_mode == "weak" and "strong" in res:
             s = res["strong"]
             line["strong"] = {"value": round(s["value"], 1), "ms_per_step": round(s["ms"], 5),

@@ -9,6 +9,8 @@
 #include "xgmi.h"
 
 namespace py = pybind11;
+
+void xgmi_fill_exchange(py::handle reducer, int bucket, XgmiExch& x);   // runtime/xgmi.cpp
 void register_comm(py::module& m);
 void register_xgmi(py::module& m);
 
@@ -225,7 +227,7 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
                 double momentum, double dampening, bool nesterov, double grad_scale,
                 std::vector<py::tuple> segs, c10::optional<at::Tensor> xg, int64_t signal_ch,
                 std::vector<int64_t> waits, double timeout_s, c10::optional<at::Tensor> bump,
-                c10::optional<py::tuple> metrics) {
+                c10::optional<py::tuple> metrics, py::object xchg, int64_t xchg_bucket) {
   c10::DeviceGuard dg(p.device());
   need(p, at::kFloat, "params");
   need(g, at::kFloat, "grads");
@@ -364,6 +366,29 @@ void optim_step(int64_t kind, at::Tensor p, at::Tensor g, at::Tensor m, c10::opt
   TORCH_CHECK(signal_ch >= -1 && signal_ch < XG_MAX_CH, "bad signal channel");
   TORCH_CHECK(a.xg != nullptr || (signal_ch < 0 && waits.empty()),
               "optimizer waits / signals need the xgmi sync words");
+  a.xx_on = 0;
+  if (!xchg.is_none()) {
+    // in-launch xgmi exchange of the slab segments (xgmi.h XgmiExch): every slab segment
+    // lies in the exchanged bucket, comes before the others (its workgroup index is its
+    // flag slot) and the slots fit
+    xgmi_fill_exchange(xchg, (int)xchg_bucket, a.xx);
+    a.xx_on = 1;
+    int64_t blk = 0;
+    bool plain_seen = false;
+    for (int i = 0; i < a.nseg; ++i) {
+      const OptSeg& sg = a.seg[i];
+      if (sg.slab == nullptr) {
+        plain_seen = true;
+        continue;
+      }
+      TORCH_CHECK(!plain_seen, "exchange: slab segments must come first");
+      TORCH_CHECK(sg.offset >= a.xx.off && sg.offset + (int64_t)sg.rows * sg.cols <= a.xx.off + a.xx.n,
+                  "exchange: a slab segment outside the exchanged bucket");
+      TORCH_CHECK(sg.wait_ch < 0, "exchange: slab segments wait for no channel");
+      blk += ((int64_t)sg.rows * sg.cols + 63) / 64;
+    }
+    TORCH_CHECK(blk <= XG_XSLOTS, "exchange: ", blk, " slab workgroups exceed ", XG_XSLOTS, " slots");
+  }
   launch_optim((int)kind, a, cur_stream(p));
 }
 
@@ -830,7 +855,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nesterov"), py::arg("grad_scale"), py::arg("segs"), py::arg("xg") = py::none(),
         py::arg("signal_ch") = -1, py::arg("waits") = std::vector<int64_t>{},
         py::arg("timeout_s") = 60.0, py::arg("bump") = py::none(),
-        py::arg("metrics") = py::none());
+        py::arg("metrics") = py::none(), py::arg("xchg") = py::none(), py::arg("xchg_bucket") = 1);
   m.def("gather_epoch", &gather_epoch, py::arg("images"), py::arg("labels"), py::arg("idx"),
         py::arg("out_images"), py::arg("out_labels"), py::arg("ctr") = py::none(),
         py::arg("step") = py::none(), py::arg("step_value") = 0, py::arg("max_wgs") = 0);
@@ -847,6 +872,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1,
         py::arg("a1g") = py::none(), py::arg("xng") = py::none(), py::arg("spe") = 0);
   m.def("fc1_fwd", &fc1_fwd);
+  m.attr("FC1_BIG_B") = FC1_BIG_B;
   m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
         py::arg("dht"), py::arg("ldt"), py::arg("slab"), py::arg("metrics"), py::arg("c0"),

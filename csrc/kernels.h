@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "xgmi.h"
+
 
 // A training step's rows in the epoch buffer.  The data-step counter c runs on across epochs
 // (nothing resets it at an epoch boundary); with spe > 0 steps per epoch the buffer holds two
@@ -127,9 +129,16 @@ struct OptArgs {
   int32_t mnslab, mcol;
   int64_t mstride;
   double* metrics;
+  // optional (xx_on): the slab segments' reduced gradients are all-reduced in-launch over
+  // xGMI (XgmiExch, xgmi.h) before their update -- the conv bucket at world size > 1
+  int xx_on;
+  XgmiExch xx;
 };
 
 void launch_optim(int kind, OptArgs& a, hipStream_t st);
+// fc1_fwd switches to 128-row blocks from this batch on (runtime.cnn_step.choose_splitk
+// sizes the split-K for the same tiles)
+constexpr int FC1_BIG_B = 2048;
 
 // World size 1: the fc1-weight update fused into fc1_bwd's weight-gradient tiles (the tile
 // is final in registers; nothing else in the step reads the fp32 weights or the bf16 [n][k]

@@ -283,10 +283,14 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 
 #endif  // PDM_WANT_FWD_REST
 #if PDM_WANT_FC1_FWD
-// ---- fc1 forward: split-K GEMM, 32 rows x 128 cols per block ----
+// ---- fc1 forward: split-K GEMM, 32 MT rows x 128 cols per block ----
 // KB = k-steps per load batch: 9 (288 k-steps = 32 batches; split factors dividing 32) or 3
 // (96 batches: split factors up to 96, so B <= 64 can put W1 on ~256 CUs instead of 32-64)
-template <int KB>
+// MT = 32-row m-tiles per block: 1, or 4 for large batches (B >= FC1_BIG_B): with 32-row
+// tiles every block streams its whole K slice of W1 from L2 for 32 rows only (B = 8192,
+// split-K 1: 256 x 2.4 MB = 604 MB of L2 reads, 80 us); 128-row tiles read W1 a quarter as
+// often and leave the pool read from HBM as the bound
+template <int KB, int MT = 1>
 __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
                                                       float* __restrict__ part, int B, int kchunk) {
@@ -295,7 +299,8 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
   // XCD-aware mapping of the 1-D grid: workgroup w runs on XCD w % 8.  When the split
   // count is a multiple of 8, every XCD owns S/8 splits (1/8 of W1's K range, for all
   // m-tiles), so each XCD's L2 holds only its slice of W1 instead of all of it.
-  const int mtiles = (B + 31) / 32, S = FEAT / kchunk;
+  constexpr int MR = 32 * MT;                      // rows per block
+  const int mtiles = (B + MR - 1) / MR, S = FEAT / kchunk;
   const int w = blockIdx.x;
   int mtile, sidx;
   if (S % 8 == 0) {
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
     sidx = w / mtiles;
     mtile = w % mtiles;
   }
-  const int b0 = mtile * 32;
+  const int b0 = mtile * MR;
   const int kbeg = sidx * kchunk;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rl = lane & 15, kg = (lane >> 4) * 8;
@@ -317,17 +322,17 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
   // lane group) are bank-conflict-free (tools/lds_bank_model.py gfx950 ds_read_b128 lane
   // groups: 592 B rows were 2 passes per read, 40 % conflict cycles in the PMC table).  Rows past B read row
   // B-1 (valid data, outputs never stored).
-  __shared__ __attribute__((aligned(16))) char at[32 * FC1_AROW];
+  __shared__ __attribute__((aligned(16))) char at[MR * FC1_AROW];
   // W1 is fragment-major (kernels.h frag_pos): the 16 x 32 fragment (n-tile, k-step) is
   // one 1-KB block and this lane's 16 B sit at lane * 8 in it
   const bf16* pb0 = wf1 + ((int64_t)((n0 >> 4) * (FEAT / 32) + (kbeg >> 5)) * 64 + lane) * 8;
   const bf16* pb1 = pb0 + (int64_t)(FEAT / 32) * 512;
-  f32x4 acc[2][2];
+  f32x4 acc[2 * MT][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2 * MT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int ACH = 32 * FC1_KB * 32 * 2 / 16;   // 16-B chunks of the A tile (1152)
+  constexpr int ACH = MR * FC1_KB * 32 * 2 / 16;   // 16-B chunks of the A tile (1152 at MT 1)
   // K in batches of FC1_KB steps: every operand load of a batch is issued before its
   // MFMAs (kchunk is a multiple of 32 * FC1_KB: the launch picks KB from the split factor)
   for (int kb = 0; kb < kchunk; kb += 32 * FC1_KB) {
@@ -353,24 +358,40 @@ __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict_
       *reinterpret_cast<uint4*>(at + row * FC1_AROW + col * 16) = av[u];
     }
     __syncthreads();
-    bf16x8 a0[FC1_KB], a1[FC1_KB];
+    if constexpr (MT == 1) {
+      bf16x8 a0[FC1_KB], a1[FC1_KB];
 #pragma unroll
-    for (int i = 0; i < FC1_KB; ++i) {
-      a0[i] = *reinterpret_cast<const bf16x8*>(at + rl * FC1_AROW + (32 * i + kg) * 2);
-      a1[i] = *reinterpret_cast<const bf16x8*>(at + (16 + rl) * FC1_AROW + (32 * i + kg) * 2);
-    }
+      for (int i = 0; i < FC1_KB; ++i) {
+        a0[i] = *reinterpret_cast<const bf16x8*>(at + rl * FC1_AROW + (32 * i + kg) * 2);
+        a1[i] = *reinterpret_cast<const bf16x8*>(at + (16 + rl) * FC1_AROW + (32 * i + kg) * 2);
+      }
 #pragma unroll
-    for (int i = 0; i < FC1_KB; ++i) {
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w0[i], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w1[i], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w0[i], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w1[i], acc[1][1], 0, 0, 0);
+      for (int i = 0; i < FC1_KB; ++i) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w0[i], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], w1[i], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w0[i], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], w1[i], acc[1][1], 0, 0, 0);
+      }
+    } else {
+      // one k-step at a time: the 2 MT A fragments of step i, then their 4 MT MFMAs
+#pragma unroll
+      for (int i = 0; i < FC1_KB; ++i) {
+        bf16x8 am[2 * MT];
+#pragma unroll
+        for (int m = 0; m < 2 * MT; ++m)
+          am[m] = *reinterpret_cast<const bf16x8*>(at + (16 * m + rl) * FC1_AROW + (32 * i + kg) * 2);
+#pragma unroll
+        for (int m = 0; m < 2 * MT; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[m], w0[i], acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[m], w1[i], acc[m][1], 0, 0, 0);
+        }
+      }
     }
     __syncthreads();   // this batch's A reads are done before the next batch's staging
   }
   float* out = part + (int64_t)sidx * B * HID;
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < 2 * MT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = b0 + 16 * mt + 4 * (lane >> 4) + r;
@@ -564,6 +585,11 @@ void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t*
 #if PDM_WANT_FC1_FWD
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st) {
+  if (B >= FC1_BIG_B) {                // 128-row blocks, 3-k-step batches (kernels.h)
+    dim3 grid(((B + 127) / 128) * splitk);
+    fc1_fwd_kernel<3, 4><<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);
+    return;
+  }
   dim3 grid(((B + 31) / 32) * splitk);
   if (32 % splitk == 0)
     fc1_fwd_kernel<9><<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk);

@@ -147,12 +147,22 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     red[rg][c4] = acc;
     const Hyper h = make_hyper<KIND>(a, lr_in, t_in);
     __syncthreads();
-    if (tid < 64 && e < numel) {
+    float gsum = 0.f;
+    if (tid < 64) {
       // a valid element's float4 group is never a clamped one
       const float* rf = reinterpret_cast<const float*>(&red[0][0]);
-      float gsum = 0.f;
 #pragma unroll
       for (int gq = 0; gq < 16; ++gq) gsum += rf[gq * 64 + tid];
+    }
+    if (a.xx_on) {
+      // world size > 1 over xGMI: this workgroup's 64 sums are all-reduced in-launch (one
+      // flag slot per workgroup) before the update -- no conv_reduce launch, no hand-off
+      __shared__ int s_xok;
+      if (!xg_exchange(a.xx, blockIdx.x, s.offset + e - a.xx.off, tid < 64 && e < numel, gsum,
+                       &s_xok))
+        return;            // a peer never arrived: error bit set, the host raises
+    }
+    if (tid < 64 && e < numel) {
       const_cast<float*>(G)[e] = gsum;              // the reduced gradient stays observable
       float m = m0, v = v0;
       const float p = update<KIND>(p0, gsum, m, v, h, a.grad_scale);

@@ -59,39 +59,37 @@ __device__ __forceinline__ void signal_peers(const XgmiArgs& a, int ph, int w, u
   }
 }
 
-// Wave 0 polls this rank's flags from every peer until each reaches `gen` (or the
-// deadline passes), then acquires; the verdict reaches every wave through LDS.
+// Every wave polls this rank's flags from every peer until each reaches `gen` (or the
+// deadline passes), then acquires for itself.  No LDS anywhere in these kernels: cnn_bwd
+// takes 163,200 of a CU's 163,840 LDS bytes, and a collective workgroup holding even one
+// LDS allocation granule on a CU keeps cnn_bwd's workgroup off that CU for the whole
+// persistent launch (256 workgroups on the remaining CUs = two rounds: cnn_bwd 17 -> 30 us at
+// B = 256, whatever the collective's width; profiles/r5/xgmi_cost).
 __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, unsigned gen,
-                                           long long deadline, int* s_ok) {
-  if (threadIdx.x < PDM_WAVE) {
-    const int lane = threadIdx.x;
-    const bool mine = lane < a.nranks && lane != a.rank;
-    const unsigned* f = a.flags[a.rank] + xg_flag_idx(a.ch, ph, mine ? lane : 0, w);
-    unsigned cause = 0;
-    for (unsigned it = 0;; ++it) {
-      // the error word is read on the first poll and every 64th: a wait that starts after
-      // any wait of this rank gave up fails at once, so one missing peer costs one timeout
-      const unsigned e = xg_poll_err(it) ? __builtin_amdgcn_readfirstlane(flag_load(a.err)) : 0u;
-      const bool arrived = !mine || (int)(flag_load(f) - gen) >= 0;
-      if (e != 0) {
-        cause = XG_ERR_FAILFAST;
-        break;
-      }
-      if (__all(arrived)) break;
-      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
-        cause = ph == 0 ? XG_ERR_PEER0 : XG_ERR_PEER1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+                                           long long deadline) {
+  const int lane = threadIdx.x & (PDM_WAVE - 1);
+  const bool mine = lane < a.nranks && lane != a.rank;
+  const unsigned* f = a.flags[a.rank] + xg_flag_idx(a.ch, ph, mine ? lane : 0, w);
+  unsigned cause = 0;
+  for (unsigned it = 0;; ++it) {
+    // the error word is read on the first poll and every 64th: a wait that starts after
+    // any wait of this rank gave up fails at once, so one missing peer costs one timeout
+    const unsigned e = xg_poll_err(it) ? __builtin_amdgcn_readfirstlane(flag_load(a.err)) : 0u;
+    const bool arrived = !mine || (int)(flag_load(f) - gen) >= 0;
+    if (e != 0) {
+      cause = XG_ERR_FAILFAST;
+      break;
     }
-    if (a.nranks > 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // buffer_inv sc0 sc1
-    if (lane == 0) {
-      *s_ok = cause == 0;
-      if (cause != 0) xg_record_error(a.err, cause);
+    if (__all(arrived)) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+      cause = ph == 0 ? XG_ERR_PEER0 : XG_ERR_PEER1;
+      break;
     }
+    __builtin_amdgcn_s_sleep(1);
   }
-  __syncthreads();
-  return *s_ok != 0;
+  if (a.nranks > 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // buffer_inv sc0 sc1
+  if (lane == 0 && cause != 0) xg_record_error(a.err, cause);
+  return cause == 0;
 }
 
 // One channel's all-reduce for workgroup w of W (its slice of every chunk) at call
@@ -104,13 +102,16 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
 #ifndef PDM_XG_DIAG
 #define PDM_XG_DIAG 0
 #endif
-template <int BATCH>
+// U: float4 indices per thread per pass (U x BATCH loads in flight before their stores): the
+// loops are latency-bound (a 4.7 MB bucket at one load in flight per lane ran at ~0.2 TB/s
+// beside cnn_bwd, so the optimizer waited for it; profiles/r5/xgmi_cost).
+template <int BATCH, int U>
 __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsigned gen,
-                                           long long deadline, int* s_ok) {
+                                           long long deadline) {
   const int tid = threadIdx.x;
   if (PDM_XG_DIAG == 1) {
     signal_peers(a, 0, w, gen);
-    return wait_peers(a, 0, w, gen, deadline, s_ok);
+    return wait_peers(a, 0, w, gen, deadline);
   }
   const int N = a.nranks, r = a.rank;
   const f32x4* src = reinterpret_cast<const f32x4*>(a.src);
@@ -125,7 +126,7 @@ __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsi
 
   // phase 0: push slice w of chunk d (two-shot) / of the bucket (one-shot) into row r
   // of rank d's stage.  Workgroups start at different peers so all N-1 links carry
-  // traffic at once; XG_BATCH loads are issued before their stores.
+  // traffic at once; U x BATCH loads are issued before their stores.
   for (int i0 = 0; i0 < N - 1; i0 += BATCH) {
     int dd[BATCH], hid[BATCH];
 #pragma unroll
@@ -135,18 +136,26 @@ __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsi
       const int len = two ? clampi(n4 - dd[b] * c4, 0, c4) : n4;
       hid[b] = i0 + b < N - 1 ? (lo + per < len ? lo + per : len) : 0;
     }
-    for (int j = lo + tid; j < lo + per; j += XG_THREADS) {
-      f32x4 v[BATCH];
+    for (int j0 = lo + tid; j0 < lo + per; j0 += XG_THREADS * U) {
+      f32x4 v[U][BATCH];
 #pragma unroll
-      for (int b = 0; b < BATCH; ++b)
-        if (j < hid[b]) v[b] = src[(two ? dd[b] * c4 : 0) + j];
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int b = 0; b < BATCH; ++b)
-        if (j < hid[b]) store_wt(rsrc(a.stage[dd[b]] + (long long)(par * N + r) * row4 * 4), j, v[b]);
+        for (int b = 0; b < BATCH; ++b) {
+          const int j = j0 + u * XG_THREADS;
+          if (j < hid[b]) v[u][b] = src[(two ? dd[b] * c4 : 0) + j];
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          const int j = j0 + u * XG_THREADS;
+          if (j < hid[b]) store_wt(rsrc(a.stage[dd[b]] + (long long)(par * N + r) * row4 * 4), j, v[u][b]);
+        }
     }
   }
   signal_peers(a, 0, w, gen);
-  if (!wait_peers(a, 0, w, gen, deadline, s_ok)) return false;
+  if (!wait_peers(a, 0, w, gen, deadline)) return false;
 
   // fixed rank-order sum of this rank's chunk (two-shot) / of the whole bucket (one-shot)
   {
@@ -156,48 +165,57 @@ __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsi
     const f32x4* own = src + base;
     const f32x4* stage = reinterpret_cast<const f32x4*>(a.stage[r]) + (long long)par * N * row4;
     const long long res = a.off + (long long)base * 4;  // float offset in the result arena
-    for (int j = lo + tid; j < hi; j += XG_THREADS) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = lo + tid; j0 < hi; j0 += XG_THREADS * U) {
+      f32x4 acc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int s0 = 0; s0 < N; s0 += BATCH) {
-        f32x4 v[BATCH];
+        f32x4 v[U][BATCH];
 #pragma unroll
-        for (int b = 0; b < BATCH; ++b) {
-          const int s = s0 + b;
-          if (s < N) v[b] = s == r ? own[j] : stage[s * row4 + j];
-        }
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int b = 0; b < BATCH; ++b)
-          if (s0 + b < N) acc = s0 + b == 0 ? v[b] : acc + v[b];
+          for (int b = 0; b < BATCH; ++b) {
+            const int s = s0 + b, j = j0 + u * XG_THREADS;
+            if (s < N && j < hi) v[u][b] = s == r ? own[j] : stage[s * row4 + j];
+          }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int b = 0; b < BATCH; ++b)
+            if (s0 + b < N) acc[u] = s0 + b == 0 ? v[u][b] : acc[u] + v[u][b];
       }
-      if (two) {
-        // all-gather push: the sum goes into every rank's result arena
-        for (int i = 0; i < N; ++i) store_wt(rsrc(a.result[(r + i + w) % N] + res), j, acc);
-      } else {
-        store_wt(rsrc(a.result[r] + res), j, acc);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * XG_THREADS;
+        if (j >= hi) continue;
+        if (two) {
+          // all-gather push: the sum goes into every rank's result arena
+          for (int i = 0; i < N; ++i) store_wt(rsrc(a.result[(r + i + w) % N] + res), j, acc[u]);
+        } else {
+          store_wt(rsrc(a.result[r] + res), j, acc[u]);
+        }
       }
     }
   }
   if (two) {
     signal_peers(a, 1, w, gen);
-    if (!wait_peers(a, 1, w, gen, deadline, s_ok)) return false;
+    if (!wait_peers(a, 1, w, gen, deadline)) return false;
   }
   return true;
 }
 
 // One collective call (bucket_ready / all_ready API): grid = the channel's workgroups.
 __global__ __launch_bounds__(XG_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
-  __shared__ int s_ok;
   const int w = blockIdx.x;
   const unsigned gen = a.gen[w] + 1;   // this workgroup's call count on this channel
   const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
-  if (!xg_channel<4>(a, w, gridDim.x, gen, deadline, &s_ok)) return;
+  if (!xg_channel<4, 2>(a, w, gridDim.x, gen, deadline)) return;
   if (threadIdx.x == 0) a.gen[w] = gen;
 }
 
 // Streamed mode (csrc/xgmi.h): `nsteps` steps x every channel in one launch, handed
 // off with the compute stream through the local READY / DONE words.
 __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs s) {
-  __shared__ int s_ok;
   const int w = blockIdx.x, tid = threadIdx.x;
   unsigned* loc = s.loc;
   unsigned step = loc[XG_LOC_LSTEP + w];
@@ -207,34 +225,31 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs 
       const XgmiArgs& a = s.ch[c];
       if (w >= a.nblk) continue;
       const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + a.timeout;
-      // wait for the compute stream to publish this step's bucket c
-      if (tid == 0) {
-        bool ok = true;
-        for (unsigned it = 0;; ++it) {
-          const unsigned e = xg_poll_err(it) ? __hip_atomic_load(loc + XG_LOC_ERR, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT) : 0u;
-          const unsigned ready = __hip_atomic_load(loc + XG_LOC_READY + c, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-          if (e != 0) {                    // this rank already gave up somewhere: fail fast
-            ok = false;
-            xg_record_error(loc + XG_LOC_ERR, XG_ERR_FAILFAST);
-            break;
-          }
-          if ((int)(ready - step) >= 0) break;
-          if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
-            ok = false;
-            xg_record_error(loc + XG_LOC_ERR, XG_ERR_READY);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+      // wait for the compute stream to publish this step's bucket c: every wave polls for
+      // itself (a wave-uniform verdict, no LDS word to broadcast it, see wait_peers)
+      bool ok = true;
+      for (unsigned it = 0;; ++it) {
+        const unsigned e = xg_poll_err(it) ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+            loc + XG_LOC_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
+        const unsigned ready = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+            loc + XG_LOC_READY + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (e != 0) {                      // this rank already gave up somewhere: fail fast
+          ok = false;
+          if ((tid & (PDM_WAVE - 1)) == 0) xg_record_error(loc + XG_LOC_ERR, XG_ERR_FAILFAST);
+          break;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        s_ok = ok;
+        if ((int)(ready - step) >= 0) break;
+        if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+          ok = false;
+          if ((tid & (PDM_WAVE - 1)) == 0) xg_record_error(loc + XG_LOC_ERR, XG_ERR_READY);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __syncthreads();
-      if (!s_ok) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (!ok) return;
       const unsigned gen = a.gen[w] + 1;
-      if (!xg_channel<2>(a, w, a.nblk, gen, deadline, &s_ok)) return;
+      if (!xg_channel<2, 4>(a, w, a.nblk, gen, deadline)) return;
       // every byte this workgroup stored for the channel is drained (write-through), and
       // every peer's bytes for its slice have arrived: count the workgroup done
       // (every result byte was stored write-through and is drained, and every peer's

@@ -106,7 +106,7 @@ class XgmiReducer {
     TORCH_CHECK(mode == "auto" || mode == "one" || mode == "two", "mode must be auto|one|two");
     arena_ = grads.numel();
     // heap layout: flags | result arena | stage of channel 0 | stage of channel 1 | ...
-    size_t off = round_up((size_t)XG_FLAG_WORDS * 4, kAlign);
+    size_t off = round_up((size_t)XG_FLAG_WORDS_ALL * 4, kAlign);
     result_off_ = off;
     off += round_up((size_t)arena_ * 4, kAlign);
     for (size_t i = 0; i < bounds.size(); i += 2) {
@@ -214,16 +214,19 @@ class XgmiReducer {
   // streamed mode: one persistent collective launch covering the next `nsteps` steps
   // (fork: ordered after the caller's stream); the step kernels hand buckets over
   // through the sync words, end() joins the caller's stream back
-  void begin(int nsteps) {
+  // nch: how many leading buckets the persistent launch carries (-1: all); the others are
+  // all-reduced in-launch by the kernels that produce them (fill_exchange)
+  void begin(int nsteps, int nch = -1) {
     TORCH_CHECK(open_ || nranks_ == 1, "open_peers() first");
     TORCH_CHECK(nsteps >= 1, "nsteps must be >= 1");
+    TORCH_CHECK(nch == -1 || (nch >= 1 && nch <= (int)ch_.size()), "bad channel count");
     hipStream_t cur = caller();
     XG_HIP_OK(hipEventRecord(ready_[0], cur));
     XG_HIP_OK(hipStreamWaitEvent(stream_, ready_[0], 0));
     XgmiStreamArgs sa{};
     for (size_t i = 0; i < ch_.size(); ++i) fill_args((int)i, sa.ch[i]);
     sa.loc = static_cast<unsigned*>(local_);
-    sa.nch = (int)ch_.size();
+    sa.nch = nch < 0 ? (int)ch_.size() : nch;
     sa.nsteps = nsteps;
     launch_xgmi_stream(sa, stream_);
     XG_HIP_OK(hipGetLastError());
@@ -298,6 +301,26 @@ class XgmiReducer {
 
   int num_buckets() const { return (int)ch_.size(); }
 
+  // the in-launch exchange of bucket i (XgmiExch, xgmi.h): its one-shot stage rows on every
+  // rank, the exchange flag slots and this rank's per-slot counters
+  void fill_exchange(int i, XgmiExch& x) const {
+    check_bucket(i);
+    const Channel& c = ch_[i];
+    TORCH_CHECK(c.mode == XG_ONE_SHOT, "the in-launch exchange needs a one-shot bucket");
+    for (int r = 0; r < XG_MAX_RANKS; ++r) {
+      char* base = static_cast<char*>(r < nranks_ ? peers_[r] : nullptr);
+      x.stage[r] = base ? reinterpret_cast<float*>(base + c.stage_off) : nullptr;
+      x.flags[r] = base ? reinterpret_cast<unsigned*>(base) : nullptr;
+    }
+    x.gen = static_cast<unsigned*>(local_) + XG_LOC_XGEN;
+    x.err = err_ptr();
+    x.off = c.start;
+    x.n = c.n;
+    x.timeout = timeout_ticks_;
+    x.rank = rank_;
+    x.nranks = nranks_;
+  }
+
  private:
   void alive() const { TORCH_CHECK(heap_ != nullptr, "xgmi reducer closed"); }
   void check_bucket(int i) const {
@@ -361,6 +384,11 @@ class XgmiReducer {
   hipEvent_t done_ = nullptr;
 };
 
+// bind.cpp's optimizer entry fills the in-launch exchange from a Python-held reducer
+void xgmi_fill_exchange(py::handle reducer, int bucket, XgmiExch& x) {
+  reducer.cast<const XgmiReducer&>().fill_exchange(bucket, x);
+}
+
 void register_xgmi(py::module& m) {
   m.attr("XG_MAX_RANKS") = XG_MAX_RANKS;
   py::class_<XgmiReducer>(m, "XgmiReducer")
@@ -374,7 +402,7 @@ void register_xgmi(py::module& m) {
       .def("all_ready", &XgmiReducer::all_ready)
       .def("wait_bucket", &XgmiReducer::wait_bucket)
       .def("finalize", &XgmiReducer::finalize)
-      .def("begin", &XgmiReducer::begin)
+      .def("begin", &XgmiReducer::begin, py::arg("nsteps"), py::arg("nch") = -1)
       .def("end", &XgmiReducer::end)
       .def("sync", &XgmiReducer::sync)
       .def("blocks", &XgmiReducer::blocks)

@@ -25,9 +25,15 @@ constexpr int XG_THREADS = 256;
 constexpr int XG_ONE_SHOT = 0;
 constexpr int XG_TWO_SHOT = 1;
 constexpr int XG_FLAG_WORDS = XG_MAX_CH * 2 * XG_MAX_RANKS * XG_MAX_WG;
+// in-launch exchange slots (XgmiExch): one flag per (source rank, slot) after the channel flags
+constexpr int XG_XSLOTS = 512;
+constexpr int XG_FLAG_WORDS_ALL = XG_FLAG_WORDS + XG_MAX_RANKS * XG_XSLOTS;
 
 __host__ __device__ constexpr int xg_flag_idx(int ch, int ph, int src, int w) {
   return ((ch * 2 + ph) * XG_MAX_RANKS + src) * XG_MAX_WG + w;
+}
+__host__ __device__ constexpr int xg_xflag_idx(int src, int slot) {
+  return XG_FLAG_WORDS + src * XG_XSLOTS + slot;
 }
 
 struct XgmiArgs {
@@ -66,7 +72,8 @@ constexpr int XG_LOC_FIRST = XG_LOC_ERR + 2;         // the first error's cause 
 constexpr int XG_LOC_READY = XG_LOC_ERR + 8;         // [XG_MAX_CH]
 constexpr int XG_LOC_DONE = XG_LOC_ERR + 16;         // [XG_MAX_CH]
 constexpr int XG_LOC_LSTEP = XG_LOC_ERR + 64;        // [XG_MAX_WG] steps run by the streamed kernel
-constexpr int XG_LOC_WORDS = XG_LOC_LSTEP + XG_MAX_WG;
+constexpr int XG_LOC_XGEN = XG_LOC_LSTEP + XG_MAX_WG;  // [XG_XSLOTS] in-launch exchange calls
+constexpr int XG_LOC_WORDS = XG_LOC_XGEN + XG_XSLOTS;
 // workgroups of the persistent launch (PDM_XG_WG: diagnostic builds)
 #ifndef PDM_XG_WG
 #define PDM_XG_WG 64
@@ -81,6 +88,24 @@ struct XgmiStreamArgs {
 };
 
 void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st);
+
+// ---- in-launch exchange: a bucket all-reduced INSIDE the kernel that produces it.
+// The optimizer's slab segments (the conv bucket at world size > 1) reduce their 64 slab
+// columns, push the 64 sums into every peer's stage row (write-through, system scope),
+// signal their slot's flag on every peer, wait for the peers' flags of the same slot and
+// sum the N rows in rank order -- a one-shot all-reduce of 256 B per workgroup with no
+// conv_reduce launch, no hand-off to the persistent collective and no wait launch in
+// between.  Stage rows are double-buffered by call parity, as the one-shot channel's.
+struct XgmiExch {
+  float* stage[XG_MAX_RANKS];     // the bucket's stage area on every rank (2 x N rows of n)
+  unsigned* flags[XG_MAX_RANKS];  // flag block on every rank (slots at xg_xflag_idx)
+  unsigned* gen;                  // this rank's per-slot call counters (XG_LOC_XGEN)
+  unsigned* err;                  // this rank's error word
+  long long off;                  // bucket start in the arena (floats)
+  long long n;                    // bucket length (floats): the stage row length
+  long long timeout;              // s_memrealtime ticks
+  int rank, nranks;
+};
 // compute side of streamed mode: READY[signal_ch] = STEP, then wait DONE[ch[i]] >= mult[i]*STEP
 void launch_xgmi_wait(unsigned* loc, int signal_ch, int nwait, const int* ch, const unsigned* mult,
                       long long timeout, hipStream_t st);
@@ -141,6 +166,75 @@ __device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mul
     __builtin_amdgcn_s_sleep(1);
   }
   if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// In-launch exchange (XgmiExch): called by EVERY thread of a workgroup that owns `slot`;
+// threads with `valid` hold one reduced value `v` of the bucket at bucket offset `bl` and
+// receive the rank-order sum over all ranks (the one-shot channel's order: same bits as
+// conv_reduce followed by the one-shot all-reduce).  False (error bit set) when a peer did
+// not arrive before the deadline; the caller must then skip its update.
+__device__ __forceinline__ bool xg_exchange(const XgmiExch& x, int slot, long long bl, bool valid,
+                                            float& v, int* s_ok) {
+  const int N = x.nranks, r = x.rank, tid = threadIdx.x;
+  if (N == 1) return true;
+  const unsigned gen = __hip_atomic_load(x.gen + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const long long par = gen & 1u;
+  if (valid) {
+    for (int i = 1; i < N; ++i) {
+      const int d = r + i < N ? r + i : r + i - N;
+      __hip_atomic_store(x.stage[d] + (par * N + r) * x.n + bl, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's pushes have landed
+  __syncthreads();
+  if (tid == 0) {
+    for (int d = 0; d < N; ++d)
+      if (d != r)
+        __hip_atomic_store(x.flags[d] + xg_xflag_idx(r, slot), gen, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (tid < 64) {
+    const int lane = tid;
+    const bool mine = lane < N && lane != r;
+    const unsigned* f = x.flags[r] + xg_xflag_idx(mine ? lane : 0, slot);
+    const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + x.timeout;
+    unsigned cause = 0;
+    for (unsigned it = 0;; ++it) {
+      const unsigned e = xg_poll_err(it) ? __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) : 0u;
+      const bool arrived = !mine || (int)(__hip_atomic_load(f, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_SYSTEM) - gen) >= 0;
+      if (e != 0) {
+        cause = XG_ERR_FAILFAST;
+        break;
+      }
+      if (__all(arrived)) break;
+      if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
+        cause = XG_ERR_PEER0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");         // system scope: the peers' rows
+    if (lane == 0) {
+      *s_ok = cause == 0;
+      if (cause != 0) xg_record_error(x.err, cause);
+    }
+  }
+  __syncthreads();
+  if (!*s_ok) return false;
+  if (valid) {
+    const float* st = x.stage[r] + par * N * x.n + bl;
+    float acc = 0.f;
+    for (int q = 0; q < N; ++q) {
+      const float u = q == r ? v : st[(long long)q * x.n];
+      acc = q == 0 ? u : acc + u;
+    }
+    v = acc;
+  }
+  if (tid == 0) __hip_atomic_store(x.gen + slot, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 #endif

@@ -41,9 +41,13 @@ KNOBS: Dict[str, tuple] = {
     "PDM_XGMI_STREAM": ("1", "structure", "0: per-bucket xgmi launches, no persistent kernel"),
     "PDM_XGMI_EARLY": ("1", "structure", "0: xgmi fc bucket after the conv backward"),
     "PDM_XGMI_OPT_WAIT": ("0", "structure", "1: optimizer workgroups wait per bucket"),
+    "PDM_XGMI_XCHG": ("1", "structure", "0: conv bucket via conv_reduce + the persistent "
+                      "collective instead of the optimizer's in-launch exchange"),
     "PDM_XGMI_TIMEOUT": ("60", "structure", "seconds any xgmi wait for a peer may take"),
     # bench.py
     "PDM_FORCE_COMM": ("0", "diag", "1: the world-size>1 chain at N=1 (1-rank communicator)"),
+    "PDM_EMULATE_WS": (None, "diag", "with PDM_FORCE_COMM=1: price an N-rank job's per-rank "
+                       "chain (fc1 update sharded over 128 / N rows, collectives stubbed)"),
     "PDM_BENCH_BACKEND": ("nccl", "rehearsal", "gloo: multi-rank bench on one GPU"),
     "PDM_BENCH_BOUNDARY": ("1", "diag", "0: no epoch boundary inside the timed window"),
     "PDM_BENCH_DEBUG": (None, "diag", "1: print the host timeline of the timed window"),

@@ -106,9 +106,11 @@ class GradReducer:
         return len(self.bounds)
 
     # -- xgmi streamed mode -------------------------------------------------------
-    def begin(self, nsteps: int) -> None:
-        """Launch the persistent collective for the next ``nsteps`` steps."""
-        self._native.begin(nsteps)
+    def begin(self, nsteps: int, nch: int | None = None) -> None:
+        """Launch the persistent collective for the next ``nsteps`` steps, carrying the first
+        ``nch`` buckets (default: all; the others are exchanged in-launch by their producer,
+        ``launch_optimizer(exchange=True)``)."""
+        self._native.begin(nsteps, -1 if nch is None else int(nch))
 
     def end(self) -> None:
         """Join the persistent collective back into the compute stream."""
@@ -120,12 +122,13 @@ class GradReducer:
                 return i
         raise ValueError(f"offset {offset} is in no bucket")
 
-    def waits_for(self, segments) -> list:
-        """Flat (channel, multiplier) per optimizer segment: wait for that segment's bucket."""
+    def waits_for(self, segments, exchanged=()) -> list:
+        """Flat (channel, multiplier) per optimizer segment: wait for that segment's bucket
+        (-1 for the buckets in `exchanged`, which the launch all-reduces itself)."""
         out = []
         for sg in segments:
             b = self.bucket_of(sg[0])
-            out += [b, self._native.blocks(b)]
+            out += [-1, 0] if b in exchanged else [b, self._native.blocks(b)]
         return out
 
     def bucket_ready(self, i: int) -> None:

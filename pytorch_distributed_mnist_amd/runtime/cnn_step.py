@@ -58,10 +58,14 @@ def frag_major_t(w: torch.Tensor) -> torch.Tensor:
     return frag_major(w.t())
 
 
+FC1_BIG_B = 2048        # csrc/kernels.h: fc1_fwd's 128-row blocks from this batch on
+
+
 def choose_splitk(B: int, cap: int = 32, target_blocks: int = 256) -> int:
-    """Split-K factor for fc1_fwd giving ~target_blocks workgroups: a divisor of 32 (every
-    split holds whole 9-step load batches of the 288 K-steps) or 48 / 96 (3-step batches)."""
-    mtiles = (B + 31) // 32
+    """Split-K factor for fc1_fwd giving ~target_blocks workgroups of (m-tile, split): 32-row
+    m-tiles, 128-row ones from B = FC1_BIG_B on; a divisor of 32 (every split holds whole
+    9-step load batches of the 288 K-steps) or 48 / 96 (3-step batches)."""
+    mtiles = (B + 31) // 32 if B < FC1_BIG_B else (B + 127) // 128
     best = 1
     for s in (1, 2, 4, 8, 16, 32, 48, 96):
         if s <= cap and mtiles * s <= target_blocks:
@@ -230,10 +234,18 @@ class CnnStep(GpuStepBase):
     def shard_supported(self, reducer=None) -> bool:
         return self.shard_unsupported_reason(reducer) is None
 
+    def shard_world_size(self, reducer=None) -> int:
+        """The world size the fc1 shard is sized for: the communicator's, or with a 1-rank
+        communicator the emulated one (StepStructure.emulate_ws, pricing runs)."""
+        red = reducer or self.reducer
+        ws = red.comm.world_size
+        emu = self.structure.emulate_ws
+        return int(emu) if (emu and ws == 1) else ws
+
     def shard_unsupported_reason(self, reducer=None):
         """None when the fc1 update can be sharded over `reducer`'s ranks, else why not."""
         red = reducer or self.reducer
-        ws = red.comm.world_size
+        ws = self.shard_world_size(red)
         if not red.active:
             return "no gradient reduction at world size 1"
         if not red.can_shard:
@@ -251,7 +263,7 @@ class CnnStep(GpuStepBase):
             if not self.shard_supported():
                 raise RuntimeError("fc1 sharding needs an RCCL or gloo data plane and a world "
                                    "size that splits 128 rows into multiples of 16")
-            ws, r = self.reducer.comm.world_size, self.reducer.comm.rank
+            ws, r = self.shard_world_size(), self.reducer.comm.rank
             rows = 128 // ws
             self.reducer.set_shard(0, self.arena.spec.offset("fc1.weight"), rows * 9216)
             self._shard_rows = (r * rows, rows)
@@ -384,7 +396,9 @@ class CnnStep(GpuStepBase):
         carry = rccl and (self.shard_fc or (self.fc_carry and not self.fc_early))
         streamed = self.reducer.streamed
         if streamed:
-            self.reducer.begin(n)        # one persistent xgmi collective for the n steps
+            # one persistent xgmi collective for the n steps (the fc bucket only when the
+            # optimizer exchanges the conv bucket itself)
+            self.reducer.begin(n, 1 if self._xchg() else None)
         for i in range(n):
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
             self.phase = (self.phase + 1) % self.phase_period
@@ -444,6 +458,13 @@ class CnnStep(GpuStepBase):
         if self.fuse_conv_reduce:
             # world_size 1: no all-reduce, the conv slab reduction runs inside the update
             self.launch_optimizer(self._fused_segments(nblk))
+            return
+        if self._xchg():
+            # xgmi streamed: the optimizer reduces the conv slabs AND all-reduces the conv
+            # bucket in-launch (each slab workgroup exchanges its 64 sums with its peers); its
+            # fc workgroups take bucket 0 from the persistent collective, which reduced it
+            # beside cnn_bwd.  No conv_reduce launch, no wait launch.
+            self.launch_optimizer(self._fused_segments(nblk), exchange=True)
             return
         C.conv_reduce(self.conv_slab, nblk, G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
@@ -524,6 +545,12 @@ class CnnStep(GpuStepBase):
         if not carry_out:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(b0)
+
+    def _xchg(self) -> bool:
+        """xgmi streamed mode with the conv bucket exchanged inside the optimizer launch."""
+        red = self.reducer
+        return (red.active and getattr(red, "kind", None) == "xgmi" and red.streamed and
+                self.structure.xgmi_exchange)
 
     def _fc_update(self):
         """fc1_bwd's fused fc1-weight SGD update (bind.cpp make_fc_update)."""

@@ -315,7 +315,7 @@ class GpuStepBase:
         return [(0, 1, self.arena.spec.total, None, None)]
 
     def launch_optimizer(self, segments=None, signal_ch: int = -1, bump=None,
-                         metrics=None) -> None:
+                         metrics=None, exchange: bool = False) -> None:
         """One fused optimizer launch over `segments` (default: every parameter).
 
         xgmi streamed mode: bucket `signal_ch` (>= 0) is published to the persistent
@@ -330,7 +330,13 @@ class GpuStepBase:
         segs = self._opt_segments if segments is None else segments
         red = self.reducer
         xg = {}
-        if red.streamed:
+        if exchange:
+            # xgmi streamed, in-launch exchange of bucket 1 (the conv slabs): its workgroups
+            # all-reduce their sums themselves; every other workgroup waits for its bucket
+            # from the persistent collective (long done by now: it ran beside cnn_bwd)
+            xg = dict(xg=red.sync, signal_ch=-1, waits=red.waits_for(segs, exchanged=(1,)),
+                      timeout_s=red.timeout_s, xchg=red._native, xchg_bucket=1)
+        elif red.streamed:
             waits = red.waits_for(segs)
             if self.structure.xgmi_opt_wait:
                 xg = dict(xg=red.sync, signal_ch=signal_ch, waits=waits, timeout_s=red.timeout_s)

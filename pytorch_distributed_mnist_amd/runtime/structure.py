@@ -37,6 +37,10 @@ class StepStructure:
     # xgmi: the fc bucket leaves right after fc1_bwd; optimizer workgroups wait per bucket
     xgmi_early: bool = True
     xgmi_opt_wait: bool = False
+    # xgmi streamed (CNN): the conv bucket all-reduced inside the optimizer launch that
+    # reduces its slabs (no conv_reduce launch, no wait launch); False: conv_reduce, the
+    # persistent collective, a wait launch
+    xgmi_exchange: bool = True
     # Linear, world size 1: the slab reduction inside the optimizer launch
     fuse_lin_reduce: bool = True
     # workgroups of the ahead-of-time epoch gather (0: one per 16 rows)
@@ -46,6 +50,10 @@ class StepStructure:
     f32_conv: str = "x3"
     f32_upw: Optional[int] = None
     f32_ipb: Optional[int] = None
+    # pricing only (PDM_EMULATE_WS, with a forced 1-rank communicator): size the sharded fc1
+    # update for this world size -- the rank updates 128 / N rows and its collectives are
+    # the 1-rank communicator's no-ops -- so an N-rank job's per-rank chain runs on one GPU
+    emulate_ws: Optional[int] = None
 
     def __post_init__(self):
         if self.rccl_mode not in RCCL_MODES:
@@ -74,10 +82,16 @@ class StepStructure:
                    bands=opt_int("PDM_BANDS"), fwd_bands=opt_int("PDM_FWD_BANDS"),
                    xgmi_early=flag("PDM_XGMI_EARLY", d.xgmi_early),
                    xgmi_opt_wait=knobs.get("PDM_XGMI_OPT_WAIT", "0") == "1",
+                   # ranks sharing one GPU (the one-GPU rehearsal): the exchange's spinning
+                   # optimizer grid would keep a peer's cnn_bwd, which needs a whole CU, off
+                   # the device until the wait times out -- the wait launch is used there
+                   xgmi_exchange=flag("PDM_XGMI_XCHG", d.xgmi_exchange) and
+                   knobs.get("PDM_SHARE_DEVICE") != "1",
                    fuse_lin_reduce=flag("PDM_FUSE_LIN_REDUCE", d.fuse_lin_reduce),
                    ahead_gather_wgs=int(knobs.get("PDM_AHEAD_GATHER_WGS", "0")),
                    f32_conv=knobs.get("PDM_F32_CONV", d.f32_conv),
-                   f32_upw=opt_int("PDM_F32_UPW"), f32_ipb=opt_int("PDM_F32_IPB"))
+                   f32_upw=opt_int("PDM_F32_UPW"), f32_ipb=opt_int("PDM_F32_IPB"),
+                   emulate_ws=opt_int("PDM_EMULATE_WS"))
 
     def with_(self, **kw) -> "StepStructure":
         return replace(self, **kw)

@@ -135,3 +135,19 @@ def test_bench_calibration_survives_failing_candidates(gpu):
     for name in ("xgmi", "rccl-early", "rccl-side"):
         assert f"{name} failed calibration" in notes, notes
     assert d["value"] > 0
+
+
+def test_bench_emulated_rank_pricing(gpu):
+    """PDM_EMULATE_WS=8 with a forced 1-rank communicator: the per-rank chain of an 8-rank job
+    at the reference's per-rank batch (256 / 8 = 32), the fc1 update sharded over 16 rows."""
+    env = dict(os.environ, PDM_FORCE_COMM="1", PDM_EMULATE_WS="8", PDM_RCCL_MODE="zero",
+               PDM_COMM="rccl")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20",
+                        "--warmup", "3", "--scaling", "weak", "--batch-per-rank", "32"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    c = d["config"]
+    assert c["emulated_world_size"] == 8 and c["fc1_update_sharded"] is True
+    assert c["grad_transport"] == "rccl-zero" and c["batch_per_rank"] == 32
+    assert d["value"] > 0

@@ -178,10 +178,12 @@ def test_cnn_forward_kernels(gpu, B):
     assert (((mask & 0x0F) & ((mask & 0x0F) - 1)) == 0).all()   # one bit at most
 
 
-@pytest.mark.parametrize("B,S", [(32, 32), (32, 96), (64, 48), (37, 96), (256, 32)])
+@pytest.mark.parametrize("B,S", [(32, 32), (32, 96), (64, 48), (37, 96), (256, 32), (2048, 16),
+                                 (2100, 4), (8192, 4)])
 def test_fc1_fwd_split_k(gpu, B, S):
     """fc1_fwd's split-K partials (9-k-step load batches for S | 32, 3-k-step batches for
-    S = 48 / 96) sum to pool . W1^T of the bf16 operands in fp32."""
+    S = 48 / 96; 128-row blocks from B = 2048 on, incl. a ragged last block) sum to
+    pool . W1^T of the bf16 operands in fp32."""
     prog, _, _ = _program(B)
     st = prog.gpu
     C = st.C
@@ -197,9 +199,11 @@ def test_fc1_fwd_split_k(gpu, B, S):
     assert rel(got, ref) < 1e-5
 
 
-@pytest.mark.parametrize("B", [64, 40, 300])
+@pytest.mark.parametrize("B", [64, 40, 300, 8192])
 def test_cnn_step_gradients_match_autograd(gpu, B):
-    prog, train, _ = _program(B)      # SGD lr=0: params unchanged, grads left in the arena
+    """One step's gradients vs fp32 autograd; B = 8192 is BASELINE config 5's per-rank batch
+    (32 images per conv-backward workgroup, fc1 split-K 1)."""
+    prog, train, _ = _program(B, n=max(600, B))   # SGD lr=0: params unchanged, grads kept
     idx = distributed_indices(len(train), 1, 0, 0)
     prog.set_train_indices(idx)
     tp = _torch_params(prog)
@@ -291,7 +295,7 @@ def test_cnn_large_batch_epoch(gpu):
     res = []
     for graphs in (True, False):
         p = build_local_program("cnn", "bf16", "cuda", 8192, train, test, optimizer="sgd",
-                                lr=0.05, momentum=0.9, seed=1, use_graphs=graphs)
+                                lr=0.01, momentum=0.9, seed=1, use_graphs=graphs)
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(n, 1, 0, 0))
         tl, ta = p.train_epoch()                 # 9 full steps + the 1000-image tail

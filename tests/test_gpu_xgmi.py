@@ -88,6 +88,15 @@ def _run_workers(nproc, tmp_path, **extra):
     return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(nproc)]
 
 
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_xgmi_optimizer_in_launch_exchange(gpu, tmp_path, nproc):
+    """The conv bucket's in-launch exchange inside the optimizer (CnnStep with the streamed
+    xgmi transport): N ranks sharing one GPU, slab segments only, against the exact rank-order
+    sum, eager and graph-replayed."""
+    for d in _run_workers(nproc, tmp_path, PDM_XGMI_UNIT="xchg"):
+        assert d["xchg_ok"], d
+
+
 def test_xgmi_two_ranks_one_gpu(gpu, tmp_path):
     for d in _run_workers(2, tmp_path):
         assert d["one"] and d["two"] and d["auto"], d

@@ -67,3 +67,21 @@ def test_occupancy_budgets(kernels):
     # fc1_bwd: 256 threads, one wave per SIMD per workgroup, all roles one round
     for k, v in _find(kernels, "fc1_bwd_kernel").items():
         assert v["vgpr_count"] + v.get("agpr_count", 0) <= 512, k
+
+
+def test_collective_kernels_fit_beside_cnn_bwd(kernels):
+    """The xgmi collectives run beside cnn_bwd, which takes 163,200 of a CU's 163,840 LDS
+    bytes: any LDS allocation of theirs would keep cnn_bwd's workgroup off their CUs for the
+    whole persistent launch (two rounds of cnn_bwd, 17 -> 30 us at B = 256).  They use none,
+    and few enough registers to share a SIMD with the two waves of the one-image cnn_bwd and
+    of the row-band kernels (512 per lane, allocated in blocks of 8)."""
+    def alloc(v):
+        return -(-(v["vgpr_count"] + v.get("agpr_count", 0)) // 8) * 8
+    beside = [v for k, v in kernels.items()
+              if "cnn_bwd_band_kernel" in k or ("cnn_bwd_kernel" in k and "ILb1E" in k)]
+    assert beside
+    free = min(512 - 2 * alloc(v) for v in beside)
+    for name in ("xgmi_stream_kernel", "xgmi_allreduce_kernel", "xgmi_wait_kernel"):
+        for k, v in _find(kernels, name).items():
+            assert v["group_segment_fixed_size"] == 0, k
+            assert alloc(v) <= free, (k, alloc(v), free)

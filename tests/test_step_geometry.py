@@ -7,14 +7,16 @@ from pytorch_distributed_mnist_amd.runtime.cnn_step import choose_splitk
 
 
 @pytest.mark.parametrize("B,cap,S", [(256, 32, 32), (32, 32, 32), (1024, 32, 8), (32, 96, 96),
-                                     (64, 96, 96), (128, 96, 48), (256, 96, 32), (37, 32, 32)])
+                                     (64, 96, 96), (128, 96, 48), (256, 96, 32), (37, 32, 32),
+                                     (2048, 32, 16), (4096, 32, 8), (8192, 32, 4)])
 def test_fc1_split_k(B, cap, S):
     """~256 workgroups of (32-row m-tile, split): a divisor of 32 (9-k-step load batches) or
     48 / 96 (3-k-step batches) within the cap."""
     s = choose_splitk(B, cap=cap)
     assert s == S
     assert 32 % s == 0 or 96 % s == 0
-    assert ((B + 31) // 32) * s <= 256 or s == 1
+    rows = 32 if B < 2048 else 128            # fc1_fwd's m-tile (kernels.h FC1_BIG_B)
+    assert ((B + rows - 1) // rows) * s <= 256 or s == 1
 
 
 @pytest.mark.parametrize("B", [1, 5, 32, 37, 64, 100, 256, 300, 1024])

@@ -82,6 +82,84 @@ def check_collective(comm, dev, rank, ws, mode):
     return bool(ok), [d["mode"] for d in desc]
 
 
+def exchange_unit(comm, dev, rank, ws):
+    """The optimizer's in-launch exchange of the conv bucket alone (slab segments only,
+    lr = 0), the part of the streamed CNN step that ranks sharing ONE GPU cannot run inside a
+    whole step (a spinning optimizer grid would keep the peer's cnn_bwd, which needs a whole
+    CU, off the device): the gradients it leaves in the result arena must equal the rank-order
+    sum of every rank's slab sums -- eager calls (both stage parities) and graph replays."""
+    from pytorch_distributed_mnist_amd.ops import _ext
+    from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
+    C = _ext.require()
+    n = FC + CONV
+    grads = torch.zeros(n, device=dev)
+    red = GradReducer(comm, grads, [(0, FC), (FC, n)], transport="xgmi")
+    assert red.kind == "xgmi"
+    SL, nslab = C.CNN_CONV_SLAB, 6
+    cols = torch.arange(SL, dtype=torch.float32)
+    base = torch.stack([((cols % 97) - 48) * (rank + 1) + j for j in range(nslab)])   # exact sums
+    slab = base.reshape(-1).to(dev).contiguous()
+    params = torch.zeros(n, device=dev)
+    mom = torch.zeros(n, device=dev)
+    lr = torch.zeros(1, dtype=torch.float64, device=dev)
+    step = torch.ones(1, dtype=torch.int64, device=dev)
+    # (arena offset, rows, cols, slab column) of conv2.weight / .bias, conv1.weight / .bias
+    parts = [(FC, 64, 288, 0), (FC + 18432, 1, 64, C.CNN_CONV_SLAB_DB2),
+             (FC + 18496, 1, 288, C.CNN_CONV_SLAB_DW1), (FC + 18816, 1, 32, C.CNN_CONV_SLAB_DB1)]
+    segs = [(off, r, c, None, None, (slab, nslab, col0, SL)) for off, r, c, col0 in parts]
+
+    def launch():
+        C.optim_step(C.OPT_SGD, params, red.out_grads, mom, None, lr, step, 0.0, 0.0, 0.0, 0.0,
+                     0.0, 0.0, False, 1.0, segs, xg=red.sync, signal_ch=-1,
+                     waits=red.waits_for(segs, exchanged=(1,)), timeout_s=red.timeout_s,
+                     xchg=red._native, xchg_bucket=1)
+
+    def expected(scale):
+        mine = (base * scale).sum(0)                   # this rank's slab sums, per column
+        tot = rank_order_sum(mine, ws)
+        want = torch.full((CONV,), float("nan"))     # nan: padding, not compared
+        for off, r, c, col0 in parts:
+            want[off - FC:off - FC + r * c] = tot[col0:col0 + r * c]
+        return want
+
+    ok = True
+    info = []
+
+    def check(tag, scale):
+        got, want = red.out_grads[FC:n].cpu(), expected(scale)
+        seg = ~torch.isnan(want)
+        good = torch.equal(got[seg], want[seg])
+        if not good:
+            bad = ((got != want) & seg).nonzero().flatten()
+            i = int(bad[0])
+            info.append(f"{tag}: {bad.numel()} wrong, first at {i}: got {float(got[i])} "
+                        f"want {float(want[i])} (err {red._xgmi.native.error()})")
+        return good
+
+    for it in range(3):                               # eager: both stage parities, twice
+        slab.copy_((base * (it + 1)).reshape(-1).to(dev))
+        launch()
+        torch.cuda.synchronize()
+        ok = check(f"eager {it}", it + 1) and ok
+        log(f"xchg eager {it} ok={ok}")
+    scale = torch.ones(1, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(3):
+            slab.mul_(scale)
+            launch()
+    for it in range(2):
+        slab.copy_(base.reshape(-1).to(dev))
+        scale.fill_(2.0)
+        g.replay()
+        torch.cuda.synchronize()
+        ok = check(f"graph {it}", 8.0) and ok
+        log(f"xchg graph {it} ok={ok}")
+    red.check()
+    red.close()
+    return {"xchg_ok": bool(ok), "xchg_info": info}
+
+
 def train_model(arch, comm, dev, rank, ws, transport):
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
@@ -207,6 +285,12 @@ def main():
     comm = TorchComm()
     res = {"rank": rank}
     absent = os.environ.get("PDM_XGMI_ABSENT")
+    if os.environ.get("PDM_XGMI_UNIT") == "xchg":
+        res.update(exchange_unit(comm, dev, rank, ws))
+        with open(os.path.join(os.environ["PDM_XGMI_OUT"], f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+        dist.destroy_process_group()
+        return
     if absent in ("1", "streamed"):
         res.update(absent_peer(comm, dev, rank, ws) if absent == "1" else
                    absent_peer_streamed(comm, dev, rank, ws))
