@@ -102,6 +102,10 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
 #ifndef PDM_XG_DIAG
 #define PDM_XG_DIAG 0
 #endif
+// float4 indices per lane per pass of the persistent kernel's loops (diagnostic builds vary it)
+#ifndef PDM_XG_U
+#define PDM_XG_U 4
+#endif
 // U: float4 indices per thread per pass (U x BATCH loads in flight before their stores): the
 // loops are latency-bound (a 4.7 MB bucket at one load in flight per lane ran at ~0.2 TB/s
 // beside cnn_bwd, so the optimizer waited for it; profiles/r5/xgmi_cost).
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (!ok) return;
       const unsigned gen = a.gen[w] + 1;
-      if (!xg_channel<2, 4>(a, w, a.nblk, gen, deadline)) return;
+      if (!xg_channel<2, PDM_XG_U>(a, w, a.nblk, gen, deadline)) return;
       // every byte this workgroup stored for the channel is drained (write-through), and
       // every peer's bytes for its slice have arrived: count the workgroup done
       // (every result byte was stored write-through and is drained, and every peer's

@@ -41,6 +41,8 @@ KNOBS: Dict[str, tuple] = {
     "PDM_XGMI_STREAM": ("1", "structure", "0: per-bucket xgmi launches, no persistent kernel"),
     "PDM_XGMI_EARLY": ("1", "structure", "0: xgmi fc bucket after the conv backward"),
     "PDM_XGMI_OPT_WAIT": ("0", "structure", "1: optimizer workgroups wait per bucket"),
+    "PDM_XGMI_OUTSIDE": ("1", "structure", "0: the persistent xgmi collective inside every "
+                         "step graph (fork / join edges) instead of launched per train_steps"),
     "PDM_XGMI_XCHG": ("1", "structure", "0: conv bucket via conv_reduce + the persistent "
                       "collective instead of the optimizer's in-launch exchange"),
     "PDM_XGMI_TIMEOUT": ("60", "structure", "seconds any xgmi wait for a peer may take"),
@@ -72,6 +74,7 @@ KNOBS: Dict[str, tuple] = {
     "PDM_ABL": (None, "build", "timing ablations"),
     "PDM_XG_WG": (None, "build", "workgroups of the persistent xgmi launch (diagnostic builds)"),
     "PDM_XG_DIAG": (None, "build", "1: xgmi flag protocol without payload (timing only)"),
+    "PDM_XG_U": (None, "build", "float4 per lane per pass in the persistent xgmi loops"),
     "PDM_DG_MTP": (None, "build", "cnn_bwd dgrad tiles per pass"),
     "PDM_DG_PFD": (None, "build", "cnn_bwd dgrad prefetch distance"),
     "PDM_HIPCC_FLAGS": (None, "build", "extra hipcc flags"),

@@ -387,18 +387,21 @@ class CnnStep(GpuStepBase):
             return None, self.ylab, fb, self.a1g, self.xng
         return self.xg, self.ylab, fb, None, None
 
-    def _train_seq(self, B: int, n: int) -> None:
+    def collective_channels(self):
+        return 1 if self._xchg() else None     # the conv bucket is exchanged by the optimizer
+
+    def _train_seq(self, B: int, n: int, collective: bool = True) -> None:
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
         rccl = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
         # sharded: the W1 all-gather and the W1^T transpose are carried past the next cnn_fwd
         carry = rccl and (self.shard_fc or (self.fc_carry and not self.fc_early))
-        streamed = self.reducer.streamed
+        streamed = self.reducer.streamed and collective
         if streamed:
             # one persistent xgmi collective for the n steps (the fc bucket only when the
             # optimizer exchanges the conv bucket itself)
-            self.reducer.begin(n, 1 if self._xchg() else None)
+            self.reducer.begin(n, self.collective_channels())
         for i in range(n):
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
             self.phase = (self.phase + 1) % self.phase_period

@@ -241,7 +241,9 @@ class GpuStepBase:
             gc.disable()
             try:
                 with torch.cuda.graph(g):          # captured on a side stream
-                    self._train_seq(B, nsteps)
+                    # the persistent collective stays out of the graph when it is launched
+                    # per train_steps call (collective_outside): no cross-queue edges
+                    self._train_seq(B, nsteps, collective=not self.collective_outside())
             finally:
                 if gc_on:
                     gc.enable()
@@ -279,7 +281,21 @@ class GpuStepBase:
         if self.use_graphs:
             k = self.GRAPH_STEPS
             r = n % k
-            for size in [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]:
+            sizes = [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]
+            if self.collective_outside():
+                # one persistent collective for all n steps, launched eagerly on its own
+                # stream beside the graph replays: the steps hand it their buckets through
+                # device words, and the last optimizer waits for its last bucket, so
+                # nothing has to join it back (a graph fork / join edge between two queues
+                # costs 5-10 us on MI355X, every replay).  Every graph is captured first: a
+                # capture synchronizes the device, which would wait for a running
+                # collective that waits for steps not yet launched.
+                ph = self.phase
+                for size in sizes:
+                    self._graph(B, size, ph)
+                    ph = (ph + size) % self.phase_period
+                self.reducer.begin(n, self.collective_channels())
+            for size in sizes:
                 self._issue_ahead()
                 self._replay(B, size)
                 self._ctr_host += size
@@ -295,11 +311,21 @@ class GpuStepBase:
     def train_step(self, B: int) -> None:
         self.train_steps(B, 1)
 
-    def _train_seq(self, B: int, n: int) -> None:
-        """n consecutive steps (captured together into one graph, or eager)."""
-        streamed = self.reducer.streamed
+    def collective_outside(self) -> bool:
+        """Streamed xgmi: the persistent collective is launched per train_steps call outside
+        the step graphs (StepStructure.xgmi_outside) instead of inside every graph."""
+        return bool(self.reducer.streamed and self.structure.xgmi_outside)
+
+    def collective_channels(self):
+        """Buckets the persistent collective carries (None: all)."""
+        return None
+
+    def _train_seq(self, B: int, n: int, collective: bool = True) -> None:
+        """n consecutive steps (captured together into one graph, or eager); `collective`:
+        launch (and join) the persistent collective for them here."""
+        streamed = self.reducer.streamed and collective
         if streamed:
-            self.reducer.begin(n)        # one persistent collective launch for the n steps
+            self.reducer.begin(n, self.collective_channels())  # one launch for the n steps
         for _ in range(n):
             self._train_impl(B)
             self.phase = (self.phase + 1) % self.phase_period

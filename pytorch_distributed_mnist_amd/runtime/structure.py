@@ -41,6 +41,9 @@ class StepStructure:
     # reduces its slabs (no conv_reduce launch, no wait launch); False: conv_reduce, the
     # persistent collective, a wait launch
     xgmi_exchange: bool = True
+    # xgmi streamed: the persistent collective launched eagerly per train_steps call, beside
+    # the graph replays, instead of inside every step graph (fork / join edges)
+    xgmi_outside: bool = True
     # Linear, world size 1: the slab reduction inside the optimizer launch
     fuse_lin_reduce: bool = True
     # workgroups of the ahead-of-time epoch gather (0: one per 16 rows)
@@ -85,6 +88,7 @@ class StepStructure:
                    # ranks sharing one GPU (the one-GPU rehearsal): the exchange's spinning
                    # optimizer grid would keep a peer's cnn_bwd, which needs a whole CU, off
                    # the device until the wait times out -- the wait launch is used there
+                   xgmi_outside=flag("PDM_XGMI_OUTSIDE", d.xgmi_outside),
                    xgmi_exchange=flag("PDM_XGMI_XCHG", d.xgmi_exchange) and
                    knobs.get("PDM_SHARE_DEVICE") != "1",
                    fuse_lin_reduce=flag("PDM_FUSE_LIN_REDUCE", d.fuse_lin_reduce),
