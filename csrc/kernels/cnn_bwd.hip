@@ -85,7 +85,14 @@ __device__ __forceinline__ int tile_off(int row, int byte) {
   return row * 128 + (byte ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 5));
 }
 
-__global__ __launch_bounds__(256) void fc1_bwd_kernel(
+// Two waves per SIMD, i.e. two workgroups per CU (<= 256 registers per lane; 162 VGPRs, no
+// spill): the 503 workgroups at B = 256 (288 dW + 192 dX + 23 head-slab) run in one round
+// instead of two.  fc1_bwd 10.0 -> 9.6 us, the B = 256 step 54.9 -> 53.9 us (interleaved A/B,
+// profiles/r5/fc1bwd_wpe2).  PDM_FC1BWD_WPE=1: the old bound (260 registers, one per CU).
+#ifndef PDM_FC1BWD_WPE
+#define PDM_FC1BWD_WPE 2
+#endif
+__global__ __launch_bounds__(256, PDM_FC1BWD_WPE) void fc1_bwd_kernel(
     const bf16* __restrict__ dh, const bf16* __restrict__ dht, int ldt,
     const bf16* __restrict__ pool, const bf16* __restrict__ wf1t, int B, float* __restrict__ gwf1,
     bf16* __restrict__ dpool, const float* __restrict__ head_slab, int head_blocks,

@@ -102,10 +102,7 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
 #ifndef PDM_XG_DIAG
 #define PDM_XG_DIAG 0
 #endif
-// float4 indices per lane per pass of the persistent kernel's loops (diagnostic builds vary it)
-#ifndef PDM_XG_U
-#define PDM_XG_U 4
-#endif
+
 // U: float4 indices per thread per pass (U x BATCH loads in flight before their stores): the
 // loops are latency-bound (a 4.7 MB bucket at one load in flight per lane ran at ~0.2 TB/s
 // beside cnn_bwd, so the optimizer waited for it; profiles/r5/xgmi_cost).
@@ -219,6 +216,11 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) 
 
 // Streamed mode (csrc/xgmi.h): `nsteps` steps x every channel in one launch, handed
 // off with the compute stream through the local READY / DONE words.
+// U: float4 per lane per pass (xg_channel).  Two widths: U = 4 (72 registers) fits beside the
+// one-image cnn_bwd and every band backward; U = 8 (128 registers, 44.9 vs 47.6 us per step
+// at B = 32 N = 1 forced) only beside the band backward of 4- and 8-row bands (B <= 85),
+// whose register use leaves room for it (tests/test_kernel_resources.py)
+template <int U>
 __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs s) {
   const int w = blockIdx.x, tid = threadIdx.x;
   unsigned* loc = s.loc;
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_stream_kernel(XgmiStreamArgs 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (!ok) return;
       const unsigned gen = a.gen[w] + 1;
-      if (!xg_channel<2, PDM_XG_U>(a, w, a.nblk, gen, deadline)) return;
+      if (!xg_channel<2, U>(a, w, a.nblk, gen, deadline)) return;
       // every byte this workgroup stored for the channel is drained (write-through), and
       // every peer's bytes for its slice have arrived: count the workgroup done
       // (every result byte was stored write-through and is drained, and every peer's
@@ -304,8 +306,11 @@ void launch_xgmi_wait(unsigned* loc, int signal_ch, int nwait, const int* ch, co
                      timeout);
 }
 
-void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st) {
+void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st, bool wide) {
   int grid = 1;
   for (int c = 0; c < s.nch; ++c) grid = s.ch[c].nblk > grid ? s.ch[c].nblk : grid;
-  hipLaunchKernelGGL(xgmi_stream_kernel, dim3(grid), dim3(XG_THREADS), 0, st, s);
+  if (wide)
+    hipLaunchKernelGGL(xgmi_stream_kernel<8>, dim3(grid), dim3(XG_THREADS), 0, st, s);
+  else
+    hipLaunchKernelGGL(xgmi_stream_kernel<4>, dim3(grid), dim3(XG_THREADS), 0, st, s);
 }

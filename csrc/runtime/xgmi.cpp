@@ -216,7 +216,7 @@ class XgmiReducer {
   // through the sync words, end() joins the caller's stream back
   // nch: how many leading buckets the persistent launch carries (-1: all); the others are
   // all-reduced in-launch by the kernels that produce them (fill_exchange)
-  void begin(int nsteps, int nch = -1) {
+  void begin(int nsteps, int nch = -1, bool wide = false) {
     TORCH_CHECK(open_ || nranks_ == 1, "open_peers() first");
     TORCH_CHECK(nsteps >= 1, "nsteps must be >= 1");
     TORCH_CHECK(nch == -1 || (nch >= 1 && nch <= (int)ch_.size()), "bad channel count");
@@ -228,7 +228,7 @@ class XgmiReducer {
     sa.loc = static_cast<unsigned*>(local_);
     sa.nch = nch < 0 ? (int)ch_.size() : nch;
     sa.nsteps = nsteps;
-    launch_xgmi_stream(sa, stream_);
+    launch_xgmi_stream(sa, stream_, wide);
     XG_HIP_OK(hipGetLastError());
     pending_ = true;
   }
@@ -402,7 +402,8 @@ void register_xgmi(py::module& m) {
       .def("all_ready", &XgmiReducer::all_ready)
       .def("wait_bucket", &XgmiReducer::wait_bucket)
       .def("finalize", &XgmiReducer::finalize)
-      .def("begin", &XgmiReducer::begin, py::arg("nsteps"), py::arg("nch") = -1)
+      .def("begin", &XgmiReducer::begin, py::arg("nsteps"), py::arg("nch") = -1,
+           py::arg("wide") = false)
       .def("end", &XgmiReducer::end)
       .def("sync", &XgmiReducer::sync)
       .def("blocks", &XgmiReducer::blocks)

@@ -87,7 +87,8 @@ struct XgmiStreamArgs {
   int nch, nsteps;
 };
 
-void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st);
+// wide: the 8-loads-per-lane variant (only beside the 4- / 8-row band backward kernels)
+void launch_xgmi_stream(const XgmiStreamArgs& s, hipStream_t st, bool wide = false);
 
 // ---- in-launch exchange: a bucket all-reduced INSIDE the kernel that produces it.
 // The optimizer's slab segments (the conv bucket at world size > 1) reduce their 64 slab

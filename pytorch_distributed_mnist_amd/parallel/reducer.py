@@ -106,11 +106,12 @@ class GradReducer:
         return len(self.bounds)
 
     # -- xgmi streamed mode -------------------------------------------------------
-    def begin(self, nsteps: int, nch: int | None = None) -> None:
+    def begin(self, nsteps: int, nch: int | None = None, wide: bool = False) -> None:
         """Launch the persistent collective for the next ``nsteps`` steps, carrying the first
         ``nch`` buckets (default: all; the others are exchanged in-launch by their producer,
-        ``launch_optimizer(exchange=True)``)."""
-        self._native.begin(nsteps, -1 if nch is None else int(nch))
+        ``launch_optimizer(exchange=True)``); `wide`: the variant with twice the loads in
+        flight, which fits only beside the small-band backward kernels."""
+        self._native.begin(nsteps, -1 if nch is None else int(nch), bool(wide))
 
     def end(self) -> None:
         """Join the persistent collective back into the compute stream."""

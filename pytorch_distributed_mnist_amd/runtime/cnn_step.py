@@ -390,6 +390,11 @@ class CnnStep(GpuStepBase):
     def collective_channels(self):
         return 1 if self._xchg() else None     # the conv bucket is exchanged by the optimizer
 
+    def collective_wide(self, B: int) -> bool:
+        # the 8-loads-per-lane collective (128 registers) fits beside the band backward of
+        # 4- and 8-row bands only (6 / 3 bands per image), not beside 12-row bands or cnn_bwd
+        return self.bands(B) >= 3
+
     def _train_seq(self, B: int, n: int, collective: bool = True) -> None:
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
         # runs while the fc gradients are still being all-reduced; the last step of the
@@ -401,7 +406,7 @@ class CnnStep(GpuStepBase):
         if streamed:
             # one persistent xgmi collective for the n steps (the fc bucket only when the
             # optimizer exchanges the conv bucket itself)
-            self.reducer.begin(n, self.collective_channels())
+            self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
         for i in range(n):
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
             self.phase = (self.phase + 1) % self.phase_period

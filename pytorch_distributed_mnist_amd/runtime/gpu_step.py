@@ -294,7 +294,7 @@ class GpuStepBase:
                 for size in sizes:
                     self._graph(B, size, ph)
                     ph = (ph + size) % self.phase_period
-                self.reducer.begin(n, self.collective_channels())
+                self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
             for size in sizes:
                 self._issue_ahead()
                 self._replay(B, size)
@@ -320,12 +320,17 @@ class GpuStepBase:
         """Buckets the persistent collective carries (None: all)."""
         return None
 
+    def collective_wide(self, B: int) -> bool:
+        """Whether the wide persistent collective fits beside this step's kernels at B."""
+        return False
+
     def _train_seq(self, B: int, n: int, collective: bool = True) -> None:
         """n consecutive steps (captured together into one graph, or eager); `collective`:
         launch (and join) the persistent collective for them here."""
         streamed = self.reducer.streamed and collective
         if streamed:
-            self.reducer.begin(n, self.collective_channels())  # one launch for the n steps
+            # one launch for the n steps
+            self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
         for _ in range(n):
             self._train_impl(B)
             self.phase = (self.phase + 1) % self.phase_period

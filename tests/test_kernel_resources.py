@@ -64,24 +64,38 @@ def test_occupancy_budgets(kernels):
     for k, v in _find(kernels, "cnn_bwd_band_kernel").items():
         assert v["group_segment_fixed_size"] <= 163840, k
         assert v["vgpr_count"] + v.get("agpr_count", 0) <= 256, k
-    # fc1_bwd: 256 threads, one wave per SIMD per workgroup, all roles one round
+    # fc1_bwd (and the fp32 program's): 256 threads, at most one wave per SIMD each
     for k, v in _find(kernels, "fc1_bwd_kernel").items():
         assert v["vgpr_count"] + v.get("agpr_count", 0) <= 512, k
+
+
+def _alloc(v):
+    return -(-(v["vgpr_count"] + v.get("agpr_count", 0)) // 8) * 8
 
 
 def test_collective_kernels_fit_beside_cnn_bwd(kernels):
     """The xgmi collectives run beside cnn_bwd, which takes 163,200 of a CU's 163,840 LDS
     bytes: any LDS allocation of theirs would keep cnn_bwd's workgroup off their CUs for the
     whole persistent launch (two rounds of cnn_bwd, 17 -> 30 us at B = 256).  They use none,
-    and few enough registers to share a SIMD with the two waves of the one-image cnn_bwd and
-    of the row-band kernels (512 per lane, allocated in blocks of 8)."""
-    def alloc(v):
-        return -(-(v["vgpr_count"] + v.get("agpr_count", 0)) // 8) * 8
-    beside = [v for k, v in kernels.items()
-              if "cnn_bwd_band_kernel" in k or ("cnn_bwd_kernel" in k and "ILb1E" in k)]
-    assert beside
-    free = min(512 - 2 * alloc(v) for v in beside)
+    and few enough registers to share a SIMD with the two waves of the backward kernel they run
+    beside (512 per lane, allocated in blocks of 8): the narrow persistent kernel beside the
+    one-image cnn_bwd and every band kernel, the wide one beside the 4- and 8-row bands."""
+    def free(pred):
+        ks = [v for k, v in kernels.items() if pred(k)]
+        assert ks
+        return min(512 - 2 * _alloc(v) for v in ks)
+    every = free(lambda k: "cnn_bwd_band_kernel" in k or ("cnn_bwd_kernel" in k and "ILb1E" in k))
+    small = free(lambda k: "cnn_bwd_band_kernelILi4E" in k or "cnn_bwd_band_kernelILi8E" in k)
     for name in ("xgmi_stream_kernel", "xgmi_allreduce_kernel", "xgmi_wait_kernel"):
         for k, v in _find(kernels, name).items():
             assert v["group_segment_fixed_size"] == 0, k
-            assert alloc(v) <= free, (k, alloc(v), free)
+            limit = small if "ILi8E" in k else every
+            assert _alloc(v) <= limit, (k, _alloc(v), limit)
+
+
+def test_fc1_bwd_two_workgroups_per_cu(kernels):
+    """fc1_bwd runs two 256-thread workgroups per CU (its 503 workgroups at B = 256 in one
+    round): <= 256 registers per lane and two LDS carves."""
+    for k, v in _find(kernels, "fc1_bwd_kernelEPKDF16b").items():
+        assert _alloc(v) <= 256, (k, _alloc(v))
+        assert 2 * v["group_segment_fixed_size"] <= 163840, k
