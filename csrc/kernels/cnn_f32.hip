@@ -1136,7 +1136,7 @@ __global__ __launch_bounds__(FT, 1) void f32_conv_bwd_kernel(
     const int tap = nn >> 1, ct = nn & 1;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16] = wacc[j][r];
+      pdm_slab_store(&out[(mt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16], wacc[j][r]);
   }
   float* red = dz;
 #pragma unroll
@@ -1148,13 +1148,12 @@ __global__ __launch_bounds__(FT, 1) void f32_conv_bwd_kernel(
   if (tid < C2) {
     float sacc = 0.f;
     for (int w = 0; w < 8; ++w) sacc += red[4096 + w * 64 + tid];
-    out[SLB_DB2 + tid] = sacc;
+    pdm_slab_store(&out[SLB_DB2 + tid], sacc);
   } else if (tid >= 64 && tid < 64 + C1 * 10) {
     const int e = tid - 64, ci = e / 10, tp = e - 10 * ci;
     float sacc = 0.f;
     for (int w = 0; w < 8; ++w) sacc += red[w * 512 + ci * 16 + tp];
-    if (tp < 9) out[SLB_DW1 + ci * 9 + tp] = sacc;
-    else out[SLB_DB1 + ci] = sacc;
+    pdm_slab_store(tp < 9 ? &out[SLB_DW1 + ci * 9 + tp] : &out[SLB_DB1 + ci], sacc);
   }
 }
 
@@ -1494,7 +1493,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     const int nn = wn0 + j, tap = nn >> 1, ct = nn & 1;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      out[(wmt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16] = wacc[j][r];
+      pdm_slab_store(&out[(wmt * 16 + 4 * g + r) * 288 + tap * 32 + ct * 16 + i16], wacc[j][r]);
   }
   float* red = reinterpret_cast<float*>(smem + XB_DH);
 #pragma unroll
@@ -1508,13 +1507,12 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     // channel tid = 8 c + j: the threads t = c + 8 k held it (fixed order over k)
     float sacc = 0.f;
     for (int k = 0; k < FT / 8; ++k) sacc += red[4096 + ((tid >> 3) + 8 * k) * 8 + (tid & 7)];
-    out[SLB_DB2 + tid] = sacc;
+    pdm_slab_store(&out[SLB_DB2 + tid], sacc);
   } else if (tid >= 64 && tid < 64 + C1 * 10) {
     const int e = tid - 64, ci = e / 10, tp = e - 10 * ci;
     float sacc = 0.f;
     for (int w = 0; w < 8; ++w) sacc += red[w * 512 + ci * 16 + tp];
-    if (tp < 9) out[SLB_DW1 + ci * 9 + tp] = sacc;
-    else out[SLB_DB1 + ci] = sacc;
+    pdm_slab_store(tp < 9 ? &out[SLB_DW1 + ci * 9 + tp] : &out[SLB_DB1 + ci], sacc);
   }
   PDM_STAMP(15);
 }
