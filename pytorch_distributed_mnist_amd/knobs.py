@@ -46,6 +46,9 @@ KNOBS: Dict[str, tuple] = {
     "PDM_XGMI_XCHG": ("1", "structure", "0: conv bucket via conv_reduce + the persistent "
                       "collective instead of the optimizer's in-launch exchange"),
     "PDM_XGMI_TIMEOUT": ("60", "structure", "seconds any xgmi wait for a peer may take"),
+    "PDM_XGMI_PROBE": ("1", "structure", "0: no child-process pre-flight of the xgmi "
+                       "peer mappings before a rank maps them itself"),
+    "PDM_XGMI_PROBE_TIMEOUT_S": ("120", "structure", "seconds the xgmi pre-flight may take"),
     # bench.py
     "PDM_FORCE_COMM": ("0", "diag", "1: the world-size>1 chain at N=1 (1-rank communicator)"),
     "PDM_EMULATE_WS": (None, "diag", "with PDM_FORCE_COMM=1: price an N-rank job's per-rank "

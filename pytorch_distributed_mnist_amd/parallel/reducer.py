@@ -38,6 +38,7 @@ import torch
 
 from ..ops import _ext
 from .comm import Communicator, RcclComm, TorchComm, release_retired, retire
+from .xgmi_probe import probe, selfcheck
 from .. import knobs
 
 TRANSPORTS = ("auto", "xgmi", "rccl")
@@ -250,6 +251,7 @@ class XgmiTransport:
     """
 
     _tags = 0
+    _preflight: dict = {}     # (world size, device) -> (ok, reason) of the child-process probe
 
     def __init__(self, comm: RcclComm, grads: torch.Tensor, bounds, timeout_s: float | None = None,
                  mode: str | None = None):
@@ -263,6 +265,31 @@ class XgmiTransport:
         flat = [b for se in bounds for b in se]
         err = None
         native = None
+
+        def agree(flag: bool) -> bool:
+            if ws > 1 and distributed_is_initialized():
+                t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+                return bool(t.item())
+            return flag
+
+        XgmiTransport._tags += 1
+        # a peer mapping that faults would end this process: try it in child processes first
+        # (xgmi_probe.py), once per process group and device (every rank builds the same
+        # sequence of transports, so the cache is the same on every rank)
+        self.preflight = "skipped"
+        if ws > 1 and knobs.get("PDM_XGMI_PROBE", "1") != "0":
+            pkey = (ws, dev)
+            if pkey in XgmiTransport._preflight:
+                self.preflight = "cached"
+            else:
+                XgmiTransport._preflight[pkey] = probe(
+                    rank, ws, dev, default_store(), f"pdm_amd/xgmi_probe/{XgmiTransport._tags}",
+                    agree, float(knobs.get("PDM_XGMI_PROBE_TIMEOUT_S", "120")))
+                self.preflight = "passed"
+            ok, why = XgmiTransport._preflight[pkey]
+            if not ok:
+                raise RuntimeError(f"xgmi pre-flight failed ({why})")
         try:
             native = C.XgmiReducer(rank, ws, dev, grads, flat, timeout_s, mode)
             handle = native.ipc_handle()
@@ -270,7 +297,6 @@ class XgmiTransport:
             err, handle = e, b""
         handles = [handle]
         if ws > 1:
-            XgmiTransport._tags += 1
             key = f"pdm_amd/xgmi/{XgmiTransport._tags}"
             store = default_store()
             store.set(f"{key}/{rank}", handle)
@@ -287,13 +313,6 @@ class XgmiTransport:
                 native.open_peers([bytes(handle)])
         self.native = native
 
-        def agree(flag: bool) -> bool:
-            if ws > 1 and distributed_is_initialized():
-                t = torch.tensor([1 if flag else 0], dtype=torch.int32)
-                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
-                return bool(t.item())
-            return flag
-
         # every rank has mapped every peer before any rank launches a collective kernel
         all_ok = agree(err is None) and agree(self._selfcheck(grads, bounds, ws, rank))
         if ws > 1 and distributed_is_initialized():
@@ -307,23 +326,7 @@ class XgmiTransport:
         self.timeout_s = timeout_s
 
     def _selfcheck(self, grads, bounds, ws, rank) -> bool:
-        result = self.native.result()
-        saved = grads.clone()
-        ok = True
-        n = grads.numel()
-        base = (torch.arange(n, device=grads.device, dtype=torch.int64) % 251 - 125).float()
-        for it in range(3):
-            grads.copy_(base * float((it + 1) * (rank + 1)))
-            self.native.all_ready()
-            self.native.finalize()
-            torch.cuda.synchronize(grads.device)
-            want = base * float((it + 1) * ws * (ws + 1) // 2)
-            for s, e in bounds:
-                ok = ok and torch.equal(result[s:e], want[s:e])
-        ok = ok and self.native.error() == 0
-        grads.copy_(saved)
-        torch.cuda.synchronize(grads.device)
-        return bool(ok)
+        return selfcheck(self.native, grads, bounds, ws, rank)
 
     # cause bits of the device error word (csrc/xgmi.h XG_ERR_*)
     CAUSES = {1: "a peer did not arrive for the reduce-scatter / push phase",

@@ -100,6 +100,8 @@ def test_xgmi_optimizer_in_launch_exchange(gpu, tmp_path, nproc):
 def test_xgmi_two_ranks_one_gpu(gpu, tmp_path):
     for d in _run_workers(2, tmp_path):
         assert d["one"] and d["two"] and d["auto"], d
+        # the child-process pre-flight ran once, before the first mapping (xgmi_probe.py)
+        assert d["preflight"] == ["passed", "cached", "cached"], d
         assert d["two_modes"] == ["two-shot", "two-shot"]
         assert d["auto_modes"] == ["one-shot", "one-shot"]       # 2 ranks: one-shot
         assert d["cnn_kinds"] == ["xgmi", "torch"]

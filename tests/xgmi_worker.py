@@ -39,6 +39,9 @@ def rank_order_sum(data, ws):
     return want
 
 
+PREFLIGHT = []
+
+
 def check_collective(comm, dev, rank, ws, mode):
     from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
     os.environ["PDM_XGMI_MODE"] = mode
@@ -48,7 +51,8 @@ def check_collective(comm, dev, rank, ws, mode):
     assert red.kind == "xgmi", red.kind
     gen = torch.Generator().manual_seed(100 + rank)
     ok = True
-    log(f"{mode}: reducer up {red._xgmi.describe}")
+    log(f"{mode}: reducer up {red._xgmi.describe} (pre-flight {red._xgmi.preflight})")
+    PREFLIGHT.append(red._xgmi.preflight)
     for _ in range(4):                                   # eager, bucket by bucket
         data = torch.randn(n, generator=gen)
         want = rank_order_sum(data, ws)
@@ -302,6 +306,7 @@ def main():
         ok, modes = check_collective(comm, dev, rank, ws, mode)
         res[mode] = ok
         res[mode + "_modes"] = modes
+    res["preflight"] = PREFLIGHT
     p_x, kind_x = train_model("cnn", comm, dev, rank, ws, "xgmi")
     p_g, kind_g = train_model("cnn", comm, dev, rank, ws, None)       # gloo data plane
     res["cnn_kinds"] = [kind_x, kind_g]
