@@ -503,6 +503,7 @@ def main():
         boundaries = -(-(a.steps - left) // spe) if a.steps > left else 0
         elapsed, imgs = timed(a.steps)
         chosen.check()
+        prog.gpu.check_device()
         prog.sync_master()
         if not torch.isfinite(arena.params).all():
             raise RuntimeError("non-finite parameters after the benchmark")

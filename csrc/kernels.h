@@ -210,6 +210,17 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
                      unsigned* c2, float* dh32, hipStream_t st);
+// fc1_fwd + the training head in one launch (cnn_fwd.hip fc1_head_kernel): its grid, or 0 when
+// (B, splitk, ldt) needs the two launches (128-row blocks, or more workgroups than the chip
+// holds at once: a head workgroup waits for every split-K workgroup).  sync: 4 zeroed words
+// (arrival count, head passes, error bit, spare) owned by the caller; timeout in
+// s_memrealtime ticks (100 MHz)
+constexpr int FC1_HEAD_MAX_GRID = 384;
+int fc1_head_grid(int B, int splitk, int ldt);
+void launch_fc1_head(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
+                     const float* bf1, const float* wf2, const float* bf2, const int32_t* ylab,
+                     __bf16* dh, __bf16* dht, int ldt, float* slab, double* metrics, int64_t* c0,
+                     int64_t* c1, unsigned* c2, unsigned* sync, long long timeout, hipStream_t st);
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,

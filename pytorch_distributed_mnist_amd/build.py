@@ -85,6 +85,7 @@ def compile_flags(abi: int, inc):
 # cnn_bwd (docs/kernels.md, tools/gpu_ab.sh).
 FILE_FLAGS = {
     "kernels/fc1_fwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "kernels/fc1_head.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "kernels/fc1_bwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "kernels/cnn_head.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }

@@ -132,6 +132,8 @@ class CnnStep(GpuStepBase):
         self.dht = torch.zeros(self.ldt * 128, dtype=bf16, device=dev)
         self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=torch.float32,
                                      device=dev)
+        # fc1_head's arrival count / head passes / error bit (the kernel re-arms the first two)
+        self.fc1_head_sync = torch.zeros(4, dtype=torch.int32, device=dev)
         self.dpool = torch.empty(B * 9216, dtype=bf16, device=dev)
         self.ipb = choose_ipb(B)
         # row-band steps (small batches): the forward hands a1 and the normalised x to the
@@ -413,6 +415,18 @@ class CnnStep(GpuStepBase):
         if streamed:
             self.reducer.end()
 
+    def fused_head(self, B: int) -> bool:
+        """fc1_fwd and the head as one launch (fc1_head) for per-rank batch B."""
+        return (self.structure.fuse_head and
+                self.C.fc1_head_grid(B, self.splitk_train, -(-B // 32) * 32) > 0)
+
+    def check_device(self) -> None:
+        """Raise if a fused fc1_head launch gave up waiting for its split-K workgroups (its
+        head then ran on incomplete partials and made the train loss NaN)."""
+        if int(self.fc1_head_sync[2].item()) != 0:
+            raise RuntimeError("fc1_head: a head workgroup timed out waiting for the split-K "
+                               "workgroups of its launch; this run's results are invalid")
+
     def _train_impl(self, B: int, carry_in: bool = False, carry_out: bool = False) -> None:
         """One training step (kernel chain in the module docstring).
 
@@ -437,10 +451,16 @@ class CnnStep(GpuStepBase):
         elif carry_in:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(self._bucket_segments()[0])
-        C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
-        C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab, True,
-                   self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
-                   self.ctr[0:1], self.opt._step_dev, xs)
+        if self.fused_head(B):
+            C.fc1_head(self.pool, self.wf1, self.part, B, S, P["fc1.bias"], P["fc2.weight"],
+                       P["fc2.bias"], self.ylab, self.dh, self.dht, ldt, self.head_slab,
+                       self.metrics.train_view(), self.ctr[0:1], self.opt._step_dev,
+                       self.fc1_head_sync, xs)
+        else:
+            C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
+            C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
+                       True, self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
+                       self.ctr[0:1], self.opt._step_dev, xs)
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.current_wf1t(), B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view(),

@@ -50,6 +50,10 @@ def make_gpu_step(prog, use_graphs: bool = True):
 
 
 class GpuStepBase:
+    def check_device(self) -> None:
+        """Raise if a kernel of this step recorded an error it could not raise itself (the
+        default: none can)."""
+
     def __init__(self, prog, use_graphs: bool):
         self.C = _ext.require()
         self.prog = prog

@@ -91,6 +91,7 @@ class TrainProgram:
                 self.gpu.train_step(tail)                     # ragged tail
             if self.sync_fn is not None:
                 self.sync_fn("training epoch")
+            self.gpu.check_device()
         else:
             buf = self.metrics.buf[0:3]
             for start, size in self._bounds:

@@ -23,6 +23,11 @@ class StepStructure:
     rccl_mode: str = "carry"
     # largest fc1_fwd split-K factor
     splitk_cap: int = 32
+    # training: fc1_fwd and the head in one launch (fc1_head) where the grid allows it.  Off:
+    # measured slower than the two launches (B = 256: 60.1-61.2 vs 53.1-53.7 us per step;
+    # B = 32: 38.9 vs 37.4-37.7; profiles/r5/fc1_head/) -- the write-through partials and
+    # the in-launch wait cost more than the kernel boundary they replace
+    fuse_head: bool = False
     # world size 1: the conv slab reduction inside the optimizer launch
     fuse_conv_reduce: bool = True
     # world size 1, SGD: fc1's update in fc1_bwd's weight-gradient tiles
@@ -78,6 +83,7 @@ class StepStructure:
         d = cls()
         return cls(rccl_mode=knobs.get("PDM_RCCL_MODE", d.rccl_mode),
                    splitk_cap=int(knobs.get("PDM_SPLITK_CAP", str(d.splitk_cap))),
+                   fuse_head=flag("PDM_FUSE_HEAD", d.fuse_head),
                    fuse_conv_reduce=flag("PDM_FUSE_CONV_REDUCE", d.fuse_conv_reduce),
                    fuse_fc1=flag("PDM_FUSE_FC1", d.fuse_fc1),
                    fc1_wt_double=flag("PDM_FC1_WT2", d.fc1_wt_double),
