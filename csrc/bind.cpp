@@ -418,12 +418,25 @@ void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* nam
   need_aligned(t.data_ptr(), 16, name);
 }
 
+static FcUpdate make_fc_update(const c10::optional<py::tuple>& t);
+
+// fc_carry (training, world size > 1, optional): the previous step's fc1-weight SGD update in
+// make_fc_update's format (shadow_t_next = the W1^T copy to write), run by extra workgroups of
+// this launch (kernels/fc_carry.h)
 void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx,
              c10::optional<at::Tensor> ctr, int64_t bfull, int64_t B, at::Tensor w1, at::Tensor b1,
              at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
              c10::optional<at::Tensor> xg, at::Tensor ylab, int64_t bands,
-             c10::optional<at::Tensor> a1g, c10::optional<at::Tensor> xng, int64_t spe) {
+             c10::optional<at::Tensor> a1g, c10::optional<at::Tensor> xng, int64_t spe,
+             c10::optional<py::tuple> fc_carry) {
   c10::DeviceGuard g(images.device());
+  const FcUpdate fcc = make_fc_update(fc_carry);
+  if (fcc.kind >= 0) {
+    TORCH_CHECK(fcc.shadow_t_next != nullptr, "fc_carry: the W1^T copy (entry 16) is required");
+    const bool training = (xg.has_value() && xg->defined()) || (a1g.has_value() && a1g->defined());
+    TORCH_CHECK(training, "fc_carry: training launches only");
+  }
+  const FcUpdate* pfcc = fcc.kind >= 0 ? &fcc : nullptr;
   TORCH_CHECK(bands == 1 || bands == 2 || bands == 3 || bands == 6, "bands must be 1, 2, 3 or 6");
   const bool gather = idx.has_value() && idx->defined();
   const bool counted = ctr.has_value() && ctr->defined();
@@ -483,12 +496,12 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
                         step_rows(bfull, pidx ? 0 : spe, nrow), (int)B, (int)bands, w1.data_ptr<float>(), b1.data_ptr<float>(),
                         ptr<__bf16>(w2), b2.data_ptr<float>(), ptr<__bf16>(pool),
                         pmask.data_ptr<uint8_t>(), pa1, pxn, pxg, ylab.data_ptr<int32_t>(),
-                        cur_stream(images));
+                        pfcc, cur_stream(images));
   } else {
     launch_cnn_fwd(images.data_ptr<uint8_t>(), labels.data_ptr<int32_t>(), pidx, nrow, pctr,
                    step_rows(bfull, pidx ? 0 : spe, nrow), (int)B, w1.data_ptr<float>(), b1.data_ptr<float>(), ptr<__bf16>(w2),
                    b2.data_ptr<float>(), ptr<__bf16>(pool), pmask.data_ptr<uint8_t>(), pxg,
-                   ylab.data_ptr<int32_t>(), cur_stream(images));
+                   ylab.data_ptr<int32_t>(), pfcc, cur_stream(images));
   }
 }
 
@@ -909,7 +922,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_fwd", &cnn_fwd, py::arg("images"), py::arg("labels"), py::arg("idx"), py::arg("ctr"),
         py::arg("bfull"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1,
-        py::arg("a1g") = py::none(), py::arg("xng") = py::none(), py::arg("spe") = 0);
+        py::arg("a1g") = py::none(), py::arg("xng") = py::none(), py::arg("spe") = 0,
+        py::arg("fc_carry") = py::none());
   m.def("fc1_fwd", &fc1_fwd);
   m.attr("FC1_BIG_B") = FC1_BIG_B;
   m.def("fc1_head", &fc1_head, py::arg("pool"), py::arg("wf1"), py::arg("part"), py::arg("B"),

@@ -194,7 +194,7 @@ constexpr int CNN_CONV_SLAB_DB1 = 18784;   // db1 [32]
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                     int64_t nrow, const int64_t* ctr, StepRows sr, int B, const float* w1, const float* b1,
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
-                    int32_t* ylab, hipStream_t st);
+                    int32_t* ylab, const FcUpdate* fcc, hipStream_t st);
 // small batches: each image over `bands` in {2, 3, 6} workgroups of 24 / bands conv2 rows
 // (cnn_fwd_band.hip); same pool / pmask / ylab as launch_cnn_fwd; training also writes the a1
 // image and the normalised x for cnn_bwd_band (a1g, xng) and / or the gathered uint8 image for
@@ -203,7 +203,9 @@ void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int
                          int64_t nrow, const int64_t* ctr, StepRows sr, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
                          __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, uint8_t* xg,
-                         int32_t* ylab, hipStream_t st);
+                         int32_t* ylab, const FcUpdate* fcc, hipStream_t st);
+// fcc (training, world size > 1): the previous step's fc1-weight SGD update, run by extra
+// workgroups of the forward launch (kernels/fc_carry.h FCC_WGS); nullptr: none
 void launch_fc1_fwd(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
                     hipStream_t st);
 void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, const float* wf2,

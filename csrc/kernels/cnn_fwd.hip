@@ -17,6 +17,7 @@
 //             partials, dh = dlogits.W2 * relu'(h) (bf16, + transposed copy for the
 //             fc1 weight-gradient GEMM), fc1 bias partials; advances step counters.
 #include "cnn_common.h"
+#include "fc_carry.h"
 
 // Translation-unit split: fc1_fwd and the head are compiled from fc1_fwd.hip / cnn_head.hip
 // (this file with PDM_FWD_TU = 1 / 2) under their own scheduler flags (build.py
@@ -52,14 +53,21 @@ constexpr int F_W = F_LUT + 512;              // fp32 w1 [288] | b1 [32] | b2 [6
 constexpr int F_TOTAL = F_W + 1536;           // 79360 B -> 2 workgroups / CU
 static_assert(2 * F_TOTAL <= 163840 && F_A1 % 128 == 0, "cnn_fwd LDS carve");
 
-template <bool TRAIN>
+// CARRY: workgroups [B, B + FCC_WGS) run the previous step's fc1 update (fc_carry.h)
+template <bool TRAIN, bool CARRY>
 __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, const StepRows sr,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
-    uint8_t* __restrict__ xg, int32_t* __restrict__ ylab) {
+    uint8_t* __restrict__ xg, int32_t* __restrict__ ylab, const FcUpdate fcc, int nconv) {
   __shared__ __attribute__((aligned(16))) char smem[F_TOTAL];
+  if constexpr (CARRY) {
+    if ((int)blockIdx.x >= nconv) {
+      fc_carry_role(fcc, blockIdx.x - nconv, gridDim.x - nconv, smem);
+      return;
+    }
+  }
   bf16x4* x3 = reinterpret_cast<bf16x4*>(smem + F_X3);
   char* a1s = smem + F_A1;
   bf16* ps = reinterpret_cast<bf16*>(smem + F_PS);
@@ -677,13 +685,19 @@ __global__ __launch_bounds__(256, 2) void fc1_head_kernel(
 void launch_cnn_fwd(const uint8_t* images, const int32_t* labels, const int32_t* idx,
                     int64_t nrow, const int64_t* ctr, StepRows sr, int B, const float* w1, const float* b1,
                     const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, uint8_t* xg,
-                    int32_t* ylab, hipStream_t st) {
+                    int32_t* ylab, const FcUpdate* fcc, hipStream_t st) {
+  if (fcc != nullptr) {        // training only (the caller carries an update between steps)
+    cnn_fwd_kernel<true, true><<<B + FCC_WGS, FWD_THREADS, 0, st>>>(
+        images, labels, idx, nrow, ctr, sr, w1, b1, w2, b2, pool, pmask, xg, ylab, *fcc, B);
+    return;
+  }
+  const FcUpdate none{};
   if (xg != nullptr)
-    cnn_fwd_kernel<true><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1, w2,
-                                                    b2, pool, pmask, xg, ylab);
+    cnn_fwd_kernel<true, false><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1,
+                                                           w2, b2, pool, pmask, xg, ylab, none, B);
   else
-    cnn_fwd_kernel<false><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1, w2,
-                                                     b2, pool, pmask, xg, ylab);
+    cnn_fwd_kernel<false, false><<<B, FWD_THREADS, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1,
+                                                            b1, w2, b2, pool, pmask, xg, ylab, none, B);
 }
 
 #endif

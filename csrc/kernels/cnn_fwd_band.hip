@@ -10,6 +10,7 @@
 // offset, which is even) and writes its slice of the pooled activations, the pool mask and
 // (training) its rows of the gathered uint8 image.
 #include "cnn_common.h"
+#include "fc_carry.h"
 
 namespace {
 
@@ -41,17 +42,26 @@ struct FwdBand {
                 "fwd band LDS (two workgroups per CU)");
 };
 
-template <int R, bool TRAIN>
+// CARRY: workgroups [nconv, nconv + FCC_WGS) run the previous step's fc1 update
+// (fc_carry.h)
+template <int R, bool TRAIN, bool CARRY>
 __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     const uint8_t* __restrict__ images, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ idx, int64_t nrow, const int64_t* __restrict__ ctr, const StepRows sr,
     const float* __restrict__ w1, const float* __restrict__ b1, const bf16* __restrict__ w2,
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
     bf16* __restrict__ a1g, bf16* __restrict__ xng, uint8_t* __restrict__ xg,
-    int32_t* __restrict__ ylab) {
+    int32_t* __restrict__ ylab, const FcUpdate fcc, int nconv) {
   using L = FwdBand<R>;
   constexpr int S = L::S;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
+  static_assert(L::TOTAL >= FCC_LDS, "carried fc1 update tiles fit the band's LDS");
+  if constexpr (CARRY) {
+    if ((int)blockIdx.x >= nconv) {
+      fc_carry_role(fcc, blockIdx.x - nconv, gridDim.x - nconv, smem);
+      return;
+    }
+  }
   bf16x4* x3 = reinterpret_cast<bf16x4*>(smem + L::X3);
   char* a1s = smem + L::A1;
   bf16* ps = reinterpret_cast<bf16*>(smem + L::PS);
@@ -248,14 +258,23 @@ template <int R>
 void launch_band(const uint8_t* images, const int32_t* labels, const int32_t* idx, int64_t nrow,
                  const int64_t* ctr, StepRows sr, int B, const float* w1, const float* b1,
                  const __bf16* w2, const float* b2, __bf16* pool, uint8_t* pmask, __bf16* a1g,
-                 __bf16* xng, uint8_t* xg, int32_t* ylab, hipStream_t st) {
+                 __bf16* xng, uint8_t* xg, int32_t* ylab, const FcUpdate* fcc, hipStream_t st) {
   const int nblk = B * FwdBand<R>::S;
+  if (fcc != nullptr) {        // training only (the caller carries an update between steps)
+    cnn_fwd_band_kernel<R, true, true><<<nblk + FCC_WGS, FTH, 0, st>>>(
+        images, labels, idx, nrow, ctr, sr, w1, b1, w2, b2, pool, pmask, a1g, xng, xg, ylab, *fcc,
+        nblk);
+    return;
+  }
+  const FcUpdate none{};
   if (a1g != nullptr || xg != nullptr)
-    cnn_fwd_band_kernel<R, true><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1, b1,
-                                                       w2, b2, pool, pmask, a1g, xng, xg, ylab);
+    cnn_fwd_band_kernel<R, true, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1,
+                                                              b1, w2, b2, pool, pmask, a1g, xng, xg,
+                                                              ylab, none, nblk);
   else
-    cnn_fwd_band_kernel<R, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1,
-                                                        b1, w2, b2, pool, pmask, a1g, xng, xg, ylab);
+    cnn_fwd_band_kernel<R, false, false><<<nblk, FTH, 0, st>>>(images, labels, idx, nrow, ctr, sr, w1,
+                                                               b1, w2, b2, pool, pmask, a1g, xng, xg,
+                                                               ylab, none, nblk);
 }
 
 }  // namespace
@@ -264,19 +283,19 @@ void launch_cnn_fwd_band(const uint8_t* images, const int32_t* labels, const int
                          int64_t nrow, const int64_t* ctr, StepRows sr, int B, int bands,
                          const float* w1, const float* b1, const __bf16* w2, const float* b2,
                          __bf16* pool, uint8_t* pmask, __bf16* a1g, __bf16* xng, uint8_t* xg,
-                         int32_t* ylab, hipStream_t st) {
+                         int32_t* ylab, const FcUpdate* fcc, hipStream_t st) {
   switch (bands) {
     case 2:
       launch_band<12>(images, labels, idx, nrow, ctr, sr, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
-                      xg, ylab, st);
+                      xg, ylab, fcc, st);
       break;
     case 3:
       launch_band<8>(images, labels, idx, nrow, ctr, sr, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
-                     xg, ylab, st);
+                     xg, ylab, fcc, st);
       break;
     case 6:
       launch_band<4>(images, labels, idx, nrow, ctr, sr, B, w1, b1, w2, b2, pool, pmask, a1g, xng,
-                     xg, ylab, st);
+                     xg, ylab, fcc, st);
       break;
     default:
       break;   // bind.cpp validates bands

@@ -27,6 +27,8 @@ KNOBS: Dict[str, tuple] = {
     "PDM_FC1_WT2": ("1", "structure", "0: the optimizer re-derives W1^T (no double buffer)"),
     "PDM_KEEP_GRADS": ("0", "diag", "1: store the fc1 weight gradient the fused update consumes"),
     "PDM_SPLITK_CAP": ("32", "structure", "largest fc1_fwd split-K factor"),
+    "PDM_FC1_CARRY_FWD": ("1", "structure", "0: world size > 1, the fc1 update in the optimizer "
+                          "launch instead of the next step's forward launch"),
     "PDM_FUSE_HEAD": ("0", "structure", "1: fc1_fwd and the training head in one launch "
                       "(fc1_head; measured slower, profiles/r5/fc1_head/)"),
     "PDM_BANDS": (None, "structure", "row bands per image in the conv backward (1 = off)"),

@@ -349,9 +349,10 @@ class CnnStep(GpuStepBase):
             self._bsegs = (b0, b1)
         return self._bsegs
 
-    def _fused_segments(self, nblk: int):
-        """Optimizer segments whose conv gradients are summed from `nblk` cnn_bwd slabs."""
-        segs = self._fused.get(nblk)
+    def _fused_segments(self, nblk: int, skip_fc1: bool = False):
+        """Optimizer segments whose conv gradients are summed from `nblk` cnn_bwd slabs
+        (skip_fc1: without the fc1 weight, whose update the next forward launch carries)."""
+        segs = self._fused.get((nblk, skip_fc1))
         if segs is None:
             if self._opt_segments is None:
                 self._opt_segments = self.optimizer_segments()
@@ -369,7 +370,8 @@ class CnnStep(GpuStepBase):
                     if not self.wt_double:
                         plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True, True, True))
                 elif name is None:
-                    plain.append(sg)
+                    if not (skip_fc1 and sg[0] == fc1_off):
+                        plain.append(sg)
                 else:
                     sg = tuple(sg) + (None,) * (9 - len(sg))
                     slab_segs.append(sg[:5] + ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),) +
@@ -377,8 +379,32 @@ class CnnStep(GpuStepBase):
             # slab segments first: their workgroups (a 256-deep reduction each) are
             # dispatched before the streaming fc updates instead of forming the tail
             segs = slab_segs + plain
-            self._fused[nblk] = segs
+            self._fused[(nblk, skip_fc1)] = segs
         return segs
+
+    def _segments_without_fc1(self):
+        if self._opt_segments is None:
+            self._opt_segments = self.optimizer_segments()
+        off = self.arena.spec.offset("fc1.weight")
+        return [sg for sg in self._opt_segments if sg[0] != off]
+
+    def _fwd_carry_on(self) -> bool:
+        """World size > 1, SGD: step k's fc1 update runs in step k+1's forward launch
+        (kernels/fc_carry.h) -- on the xgmi in-launch-exchange step and the RCCL nocarry step."""
+        red = self.reducer
+        if not (red.active and self.structure.fc1_carry_fwd and self.opt.kind == "sgd") or \
+                self.shard_fc:
+            return False
+        if self._xchg():
+            return True
+        return (getattr(red, "kind", None) == "rccl" and getattr(red, "_native", None) is not None
+                and not self.fc_carry and not self.fc_early)
+
+    def _fc_carry(self):
+        """The carried fc1 update (cnn_fwd fc_carry): the fused update's arguments, reading the
+        all-reduced gradient, writing the single W1^T copy."""
+        u = self._fc_update()
+        return u[:16] + (self.wf1t,)
 
     def fwd_outputs(self, B: int):
         """cnn_fwd's training outputs for per-rank batch B: (xg, ylab, bands, a1g, xng) -- the
@@ -404,13 +430,16 @@ class CnnStep(GpuStepBase):
         rccl = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
         # sharded: the W1 all-gather and the W1^T transpose are carried past the next cnn_fwd
         carry = rccl and (self.shard_fc or (self.fc_carry and not self.fc_early))
+        # world size > 1, SGD: each step's fc1 update runs in the next step's forward launch
+        fwd = self._fwd_carry_on()
         streamed = self.reducer.streamed and collective
         if streamed:
             # one persistent xgmi collective for the n steps (the fc bucket only when the
             # optimizer exchanges the conv bucket itself)
             self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
         for i in range(n):
-            self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1)
+            self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1,
+                             fwd_in=fwd and i > 0, fwd_out=fwd and i < n - 1)
             self.phase = (self.phase + 1) % self.phase_period
         if streamed:
             self.reducer.end()
@@ -427,12 +456,15 @@ class CnnStep(GpuStepBase):
             raise RuntimeError("fc1_head: a head workgroup timed out waiting for the split-K "
                                "workgroups of its launch; this run's results are invalid")
 
-    def _train_impl(self, B: int, carry_in: bool = False, carry_out: bool = False) -> None:
+    def _train_impl(self, B: int, carry_in: bool = False, carry_out: bool = False,
+                    fwd_in: bool = False, fwd_out: bool = False) -> None:
         """One training step (kernel chain in the module docstring).
 
         carry_in: the previous step's fc-bucket optimizer update is still pending; it runs
         after this step's cnn_fwd (which only needs the conv weights), so the previous fc
         all-reduce overlaps cnn_fwd.  carry_out: leave this step's fc update to the next step.
+        fwd_in / fwd_out: the same for the fc1 weight alone, whose pending update runs INSIDE
+        this step's forward launch (_fwd_carry_on).
         """
         C, P, G = self.C, self.P, self.G
         red = self.reducer
@@ -442,7 +474,8 @@ class CnnStep(GpuStepBase):
         bands = self.bands(B)
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
-                  self.pmask, *self.fwd_outputs(B), spe=self.spe)
+                  self.pmask, *self.fwd_outputs(B), spe=self.spe,
+                  fc_carry=self._fc_carry() if fwd_in else None)
         if carry_in and self.shard_fc:
             self.reducer.wait_gather()                # this step's W1 rows from every rank
             self.launch_optimizer(self._shard_segments()[1])
@@ -492,7 +525,7 @@ class CnnStep(GpuStepBase):
             # bucket in-launch (each slab workgroup exchanges its 64 sums with its peers); its
             # fc workgroups take bucket 0 from the persistent collective, which reduced it
             # beside cnn_bwd.  No conv_reduce launch, no wait launch.
-            self.launch_optimizer(self._fused_segments(nblk), exchange=True)
+            self.launch_optimizer(self._fused_segments(nblk, skip_fc1=fwd_out), exchange=True)
             return
         C.conv_reduce(self.conv_slab, nblk, G["conv2.weight"], G["conv2.bias"],
                       G["conv1.weight"], G["conv1.bias"])
@@ -548,9 +581,10 @@ class CnnStep(GpuStepBase):
             return
         if not self.fc_carry:
             # one grouped RCCL launch for both buckets, one optimizer launch for everything
+            # (but the fc1 weight when the next forward carries its update)
             self.reducer.all_ready()
             self.reducer.finalize()
-            self.launch_optimizer()
+            self.launch_optimizer(self._segments_without_fc1() if fwd_out else None)
             return
         b0, b1 = self._bucket_segments()
         self.reducer.bucket_ready(1)

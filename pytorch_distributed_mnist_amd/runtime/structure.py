@@ -23,6 +23,10 @@ class StepStructure:
     rccl_mode: str = "carry"
     # largest fc1_fwd split-K factor
     splitk_cap: int = 32
+    # world size > 1, SGD (the xgmi in-launch-exchange and RCCL nocarry steps): step k's fc1
+    # update runs in extra workgroups of step k+1's forward launch instead of the optimizer
+    # (kernels/fc_carry.h); the last step of a sequence updates in its own optimizer
+    fc1_carry_fwd: bool = True
     # training: fc1_fwd and the head in one launch (fc1_head) where the grid allows it.  Off:
     # measured slower than the two launches (B = 256: 60.1-61.2 vs 53.1-53.7 us per step;
     # B = 32: 38.9 vs 37.4-37.7; profiles/r5/fc1_head/) -- the write-through partials and
@@ -84,6 +88,7 @@ class StepStructure:
         return cls(rccl_mode=knobs.get("PDM_RCCL_MODE", d.rccl_mode),
                    splitk_cap=int(knobs.get("PDM_SPLITK_CAP", str(d.splitk_cap))),
                    fuse_head=flag("PDM_FUSE_HEAD", d.fuse_head),
+                   fc1_carry_fwd=flag("PDM_FC1_CARRY_FWD", d.fc1_carry_fwd),
                    fuse_conv_reduce=flag("PDM_FUSE_CONV_REDUCE", d.fuse_conv_reduce),
                    fuse_fc1=flag("PDM_FUSE_FC1", d.fuse_fc1),
                    fc1_wt_double=flag("PDM_FC1_WT2", d.fc1_wt_double),

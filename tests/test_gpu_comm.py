@@ -105,6 +105,44 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
     assert torch.equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("transport,B", [("rccl", 32), ("rccl", 256), ("xgmi", 32), ("xgmi", 256)])
+def test_fc1_update_carried_into_forward_is_bit_identical(gpu, transport, B):
+    """World size > 1 (forced 1-rank communicator; RCCL nocarry and the xgmi in-launch-exchange
+    step): step k's fc1 update runs in extra workgroups of step k+1's forward launch
+    (kernels/fc_carry.h) instead of the optimizer.  Weights, momentum and both bf16 copies of W1
+    must equal the optimizer-run update, over graph-captured 8-step sequences (7 carried
+    updates each), a sequence of one and the ragged tail."""
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.runtime.program import build_local_program
+    train = synthetic_split(B * 9 + 40, True)
+    test = synthetic_split(256, False)
+    out = []
+    for carry in (False, True):
+        comm = _comm(gpu)
+        p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.05,
+                                momentum=0.9, seed=4, use_graphs=True, comm=comm, force_comm=True,
+                                transport=transport)
+        assert p.reducer.kind == transport
+        if transport == "rccl":
+            p.gpu.set_rccl_mode("nocarry")
+        p.gpu.structure = p.gpu.structure.with_(fc1_carry_fwd=carry)
+        p.gpu.invalidate_graphs()
+        assert p.gpu._fwd_carry_on() == carry
+        p.optimizer.sync_hyperparams()
+        p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        p.train_epoch()
+        torch.cuda.synchronize()
+        p.reducer.check()
+        o = p.optimizer
+        out.append((p.arena.params.clone(), o.momentum_buffer.clone(), p.gpu.wf1.clone(),
+                    p.gpu.wf1t.clone()))
+        p.reducer.close()
+        comm.close()
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
 def test_rccl_comm_count(gpu):
     comm = _comm(gpu)
     assert comm.comm_count() == 1
