@@ -281,6 +281,7 @@ def main():
     comm.broadcast_(arena.params, 0)
     opt = build_optimizer(optname, arena, SimpleNamespace(lr=lr, momentum=0.9, weight_decay=1e-4))
     bounds = spec.bucket_bounds()
+    channels = spec.channel_bounds()     # the xGMI transport's finer cut (fc1.weight alone)
     # Gradient transports to choose from: with $PDM_COMM unset (auto) on the RCCL data plane
     # both the direct xGMI all-reduce and RCCL are built, and a short untimed calibration
     # run of the real step picks the faster one for this N and batch (agreed over ranks).
@@ -290,14 +291,15 @@ def main():
     if (ws > 1 or force_comm) and want == "auto" and isinstance(comm, parallel.RcclComm):
         try:
             reducers["xgmi"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
-                                                    transport="xgmi")
+                                                    transport="xgmi", channels=channels)
         except Exception as e:                # collective decision: no rank uses xgmi
             notes.append(f"xgmi unavailable: {e}")
             print(f"bench.py: xgmi transport unavailable: {e}", file=sys.stderr, flush=True)
         reducers["rccl"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
                                                 transport="rccl")
     else:
-        r0 = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm, transport=want)
+        r0 = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm, transport=want,
+                                  channels=channels)
         reducers[r0.kind] = r0
         if r0.transport_note:
             notes.append(r0.transport_note)

@@ -428,9 +428,22 @@ void cnn_fwd(at::Tensor images, at::Tensor labels, c10::optional<at::Tensor> idx
              at::Tensor w2, at::Tensor b2, at::Tensor pool, at::Tensor pmask,
              c10::optional<at::Tensor> xg, at::Tensor ylab, int64_t bands,
              c10::optional<at::Tensor> a1g, c10::optional<at::Tensor> xng, int64_t spe,
-             c10::optional<py::tuple> fc_carry) {
+             c10::optional<py::tuple> fc_carry, c10::optional<py::tuple> fc_carry_wait) {
   c10::DeviceGuard g(images.device());
-  const FcUpdate fcc = make_fc_update(fc_carry);
+  FcUpdate fcc = make_fc_update(fc_carry);
+  if (fc_carry_wait.has_value()) {
+    // (xgmi sync words, channel, multiplier, timeout_s): the carried update waits for the
+    // channel holding its gradient (kernels/fc_carry.h)
+    const py::tuple& w = *fc_carry_wait;
+    TORCH_CHECK(fcc.kind >= 0 && w.size() == 4, "fc_carry_wait: (sync, channel, mult, timeout_s) "
+                "with fc_carry");
+    fcc.wloc = opt_sync(w[0].cast<at::Tensor>());
+    fcc.wch = (int)w[1].cast<int64_t>();
+    fcc.wmult = (unsigned)w[2].cast<int64_t>();
+    fcc.wtimeout = (long long)(w[3].cast<double>() * 1e8);
+    TORCH_CHECK(fcc.wloc != nullptr && fcc.wch >= 0 && fcc.wch < XG_MAX_CH && fcc.wmult >= 1,
+                "fc_carry_wait: bad channel / multiplier");
+  }
   if (fcc.kind >= 0) {
     TORCH_CHECK(fcc.shadow_t_next != nullptr, "fc_carry: the W1^T copy (entry 16) is required");
     const bool training = (xg.has_value() && xg->defined()) || (a1g.has_value() && a1g->defined());
@@ -923,7 +936,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bfull"), py::arg("B"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("pool"), py::arg("pmask"), py::arg("xg"), py::arg("ylab"), py::arg("bands") = 1,
         py::arg("a1g") = py::none(), py::arg("xng") = py::none(), py::arg("spe") = 0,
-        py::arg("fc_carry") = py::none());
+        py::arg("fc_carry") = py::none(), py::arg("fc_carry_wait") = py::none());
   m.def("fc1_fwd", &fc1_fwd);
   m.attr("FC1_BIG_B") = FC1_BIG_B;
   m.def("fc1_head", &fc1_head, py::arg("pool"), py::arg("wf1"), py::arg("part"), py::arg("B"),

@@ -167,6 +167,12 @@ struct FcUpdate {
   // 0: the fused update consumes the gradient in registers and the fp32 fc1-weight gradient
   // is not stored (4.7 MB of writes saved per step; nothing reads it); 1: stored as usual
   int store_grad;
+  // carried update (kernels/fc_carry.h), xgmi streamed mode: wait until DONE[wch] >=
+  // wmult * STEP in the local sync words `wloc` before reading g (nullptr: no wait)
+  unsigned* wloc;
+  int wch;
+  unsigned wmult;
+  long long wtimeout;     // s_memrealtime ticks
 };
 
 // ---------------------------------------------------------------- CNN (bf16)

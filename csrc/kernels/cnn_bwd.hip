@@ -748,7 +748,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) char smem[B_TOTAL];
   // xgmi streamed mode: this kernel starting means fc1_bwd finished, i.e. the fc
   // gradient bucket is complete -> hand it to the persistent collective (csrc/xgmi.h)
-  if (xg_sync != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xg_signal_ready(xg_sync, 0);
+  if (xg_sync != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xg_signal_backward(xg_sync);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
   constexpr int S = L::S;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
   // xgmi streamed mode: fc1_bwd has finished, so the fc gradient bucket is complete
-  if (xg_sync != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xg_signal_ready(xg_sync, 0);
+  if (xg_sync != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xg_signal_backward(xg_sync);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;

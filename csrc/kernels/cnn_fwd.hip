@@ -62,6 +62,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     const float* __restrict__ b2, bf16* __restrict__ pool, uint8_t* __restrict__ pmask,
     uint8_t* __restrict__ xg, int32_t* __restrict__ ylab, const FcUpdate fcc, int nconv) {
   __shared__ __attribute__((aligned(16))) char smem[F_TOTAL];
+  static_assert(F_TOTAL >= FCC_LDS + 4, "carried fc1 update tiles fit the forward's LDS");
   if constexpr (CARRY) {
     if ((int)blockIdx.x >= nconv) {
       fc_carry_role(fcc, blockIdx.x - nconv, gridDim.x - nconv, smem);

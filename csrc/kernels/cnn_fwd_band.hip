@@ -55,7 +55,7 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
   using L = FwdBand<R>;
   constexpr int S = L::S;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
-  static_assert(L::TOTAL >= FCC_LDS, "carried fc1 update tiles fit the band's LDS");
+  static_assert(L::TOTAL >= FCC_LDS + 4, "carried fc1 update tiles fit the band's LDS");
   if constexpr (CARRY) {
     if ((int)blockIdx.x >= nconv) {
       fc_carry_role(fcc, blockIdx.x - nconv, gridDim.x - nconv, smem);

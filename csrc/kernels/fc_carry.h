@@ -15,6 +15,7 @@
 #pragma once
 #include "cnn_common.h"
 #include "optim_common.h"
+#include "xgmi.h"
 
 namespace cnn {
 
@@ -26,8 +27,22 @@ constexpr int FCC_LDS = 2 * FCC_TC * (FCC_TR + 8) * 2;         // two transpose 
 // profiles/r5/fc1_carry/)
 constexpr int FCC_WGS = FCC_TILES / 4;
 
-// workgroup wg of nwg (512 threads); smem: FCC_LDS bytes of the launch's LDS
+// workgroup wg of nwg (512 threads); smem: FCC_LDS + 4 bytes of the launch's LDS
 __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg, char* smem) {
+  // xgmi streamed mode: the fc1-weight channel may still be travelling (the optimizer no
+  // longer waits for it).  One lane polls its DONE count, the workgroup follows it through a
+  // barrier, and the gradient is then read with sc1 loads (past this CU's L1) instead of
+  // behind an acquire: every byte of it was stored write-through and drained before the
+  // collective's workgroups added to DONE (MI355X_MICROARCH.md, the sc1 hand-off table)
+  const bool sc1 = u.wloc != nullptr;
+  if (sc1) {
+    int* s_ok = reinterpret_cast<int*>(smem + FCC_LDS);
+    if (threadIdx.x == 0) *s_ok = xg_wait_done(u.wloc, u.wch, u.wmult, u.wtimeout, /*acquire=*/false);
+    __syncthreads();
+    if (!*s_ok) return;     // a peer never arrived: error bit set, the host raises
+  }
+  const __amdgpu_buffer_rsrc_t grs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(u.g), 0, 0x7fffffff, 0x00020000);
   const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
   bf16 (*tile)[FCC_TR + 8] =
       reinterpret_cast<bf16 (*)[FCC_TR + 8]>(smem + half * FCC_TC * (FCC_TR + 8) * 2);
@@ -45,7 +60,10 @@ __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const float4 p4 = *reinterpret_cast<const float4*>(u.p + e + 4 * q);
-        const float4 g4 = *reinterpret_cast<const float4*>(u.g + e + 4 * q);
+        const float4 g4 =
+            sc1 ? __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                      grs, (int)((e + 4 * q) * 4), 0, 16))                   // aux 16: sc1
+                : *reinterpret_cast<const float4*>(u.g + e + 4 * q);
         const float4 m4 = *reinterpret_cast<const float4*>(u.m + e + 4 * q);
         pv[4 * q] = p4.x; pv[4 * q + 1] = p4.y; pv[4 * q + 2] = p4.z; pv[4 * q + 3] = p4.w;
         gv[4 * q] = g4.x; gv[4 * q + 1] = g4.y; gv[4 * q + 2] = g4.z; gv[4 * q + 3] = g4.w;

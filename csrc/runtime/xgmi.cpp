@@ -235,6 +235,16 @@ class XgmiReducer {
 
   void end() { finalize(); }
 
+  // how many leading channels the conv backward publishes (those of the first bucket)
+  void set_backward_channels(int n) {
+    alive();
+    TORCH_CHECK(n >= 1 && n <= (int)ch_.size(), "backward channels: 1..", ch_.size());
+    const unsigned v = (unsigned)n;
+    XG_HIP_OK(hipSetDevice(device_));
+    XG_HIP_OK(hipMemcpy(static_cast<unsigned*>(local_) + XG_LOC_NPUB, &v, sizeof(v),
+                        hipMemcpyHostToDevice));
+  }
+
   at::Tensor sync() const {
     alive();
     auto opts = at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device_);
@@ -406,6 +416,7 @@ void register_xgmi(py::module& m) {
            py::arg("wide") = false)
       .def("end", &XgmiReducer::end)
       .def("sync", &XgmiReducer::sync)
+      .def("set_backward_channels", &XgmiReducer::set_backward_channels)
       .def("blocks", &XgmiReducer::blocks)
       .def("error", &XgmiReducer::error)
       .def("first_error", &XgmiReducer::first_error)

@@ -69,6 +69,7 @@ constexpr int XG_LOC_GEN = 0;                        // [XG_MAX_CH][XG_MAX_WG] c
 constexpr int XG_LOC_ERR = XG_MAX_CH * XG_MAX_WG;    // error bits (XG_ERR_*)
 constexpr int XG_LOC_STEP = XG_LOC_ERR + 1;          // step generation
 constexpr int XG_LOC_FIRST = XG_LOC_ERR + 2;         // the first error's cause bit (set once)
+constexpr int XG_LOC_NPUB = XG_LOC_ERR + 3;          // channels the backward publishes (0: 1)
 constexpr int XG_LOC_READY = XG_LOC_ERR + 8;         // [XG_MAX_CH]
 constexpr int XG_LOC_DONE = XG_LOC_ERR + 16;         // [XG_MAX_CH]
 constexpr int XG_LOC_LSTEP = XG_LOC_ERR + 64;        // [XG_MAX_WG] steps run by the streamed kernel
@@ -137,6 +138,16 @@ __device__ __forceinline__ bool xg_poll_err(unsigned it) { return (it & 63u) == 
 __device__ __forceinline__ void xg_signal_ready(unsigned* loc, int ch) {
   const unsigned g = __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(loc + XG_LOC_READY + ch, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The conv backward's first workgroup: the first bucket (the fc bucket, whose gradients
+// fc1_bwd finished) is complete -- publish its channels [0, NPUB) (a bucket may be cut into
+// several channels: models/specs.py channel_bounds)
+__device__ __forceinline__ void xg_signal_backward(unsigned* loc) {
+  const unsigned g = __hip_atomic_load(loc + XG_LOC_STEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned n = __hip_atomic_load(loc + XG_LOC_NPUB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (unsigned c = 0; c < (n ? n : 1u) && c < (unsigned)XG_MAX_CH; ++c)
+    __hip_atomic_store(loc + XG_LOC_READY + c, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One lane polls DONE[ch] until it reaches mult * STEP (bounded), then (acquire) an

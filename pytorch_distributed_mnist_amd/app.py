@@ -141,7 +141,8 @@ def run(args):
                              synthetic_size=args.synthetic_size)
     test_split = load_split(args.root, False, synthetic=args.synthetic)
     reducer = parallel.GradReducer(comm, arena.grads, spec.bucket_bounds(),
-                                   transport=getattr(args, "comm", None))
+                                   transport=getattr(args, "comm", None),
+                                   channels=spec.channel_bounds())
     dtype = resolve_dtype(args.dtype, args.arch, device)
     program = TrainProgram(args.arch, dtype, arena, optimizer, reducer, train_split, test_split,
                            args.batch_size, use_graphs=args.graphs)

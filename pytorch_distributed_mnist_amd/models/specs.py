@@ -39,6 +39,9 @@ class ParamSpec:
     to_internal: Callable[[torch.Tensor], torch.Tensor] = _identity
     to_torch: Callable[[torch.Tensor], torch.Tensor] = _identity
     bucket: int = 0
+    # a channel of its own inside its bucket (channel_bounds): the direct xGMI transport
+    # reduces it separately, so its consumers can wait for it alone
+    own_channel: bool = False
 
     @property
     def numel(self) -> int:
@@ -91,6 +94,25 @@ class ModelSpec:
             bounds.append((start, end))
         return bounds
 
+    def channel_bounds(self) -> Tuple[List[Tuple[int, int]], List[List[int]]]:
+        """Buckets cut further at the parameters that take a channel of their own: ([(start,
+        end)] of every channel in arena order, [channel indices of bucket b])."""
+        chans, of_bucket = [], []
+        for b, (bs, be) in enumerate(self.bucket_bounds()):
+            cuts = [bs]
+            for i, p in enumerate(self.params):
+                if p.bucket == b and p.own_channel:
+                    lo = self.offsets[i]
+                    hi = self.offsets[i + 1] if i + 1 < len(self.params) else self.total
+                    cuts += [lo, min(hi, be)]
+            cuts.append(be)
+            pts = sorted(set(cuts))
+            of_bucket.append([])
+            for lo, hi in zip(pts, pts[1:]):
+                of_bucket[-1].append(len(chans))
+                chans.append((lo, hi))
+        return chans, of_bucket
+
     @property
     def num_params(self) -> int:
         return sum(p.numel for p in self.params)
@@ -130,12 +152,16 @@ def _conv1_to_torch(t):
 def cnn_spec() -> ModelSpec:
     # Bucket 0 = fc2 + fc1 (ready right after the fc1 backward GEMM, ~4.7 MB);
     # bucket 1 = conv2 + conv1 (ready after the fused conv backward kernel).
+    # fc1.weight comes last in bucket 0, in a channel of its own: the xGMI transport reduces
+    # the small fc parameters (fc2, fc1.bias) apart from it, so the optimizer waits only for
+    # them while fc1.weight's 4.7 MB keep travelling until the next forward launch, which
+    # carries its update (kernels/fc_carry.h)
     return ModelSpec("cnn", [
         ParamSpec("fc2.weight", (10, 128), (10, 128), 6, bucket=0),
         ParamSpec("fc2.bias", (10,), (10,), 7, bucket=0),
-        ParamSpec("fc1.weight", (128, 9216), (128, 12, 12, 64), 4,
-                  _fc1_to_internal, _fc1_to_torch, bucket=0),
         ParamSpec("fc1.bias", (128,), (128,), 5, bucket=0),
+        ParamSpec("fc1.weight", (128, 9216), (128, 12, 12, 64), 4,
+                  _fc1_to_internal, _fc1_to_torch, bucket=0, own_channel=True),
         ParamSpec("conv2.weight", (64, 32, 3, 3), (64, 3, 3, 32), 2,
                   _conv2_to_internal, _conv2_to_torch, bucket=1),
         ParamSpec("conv2.bias", (64,), (64,), 3, bucket=1),

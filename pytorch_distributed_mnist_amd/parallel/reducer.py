@@ -53,11 +53,17 @@ def default_transport() -> str:
 
 class GradReducer:
     def __init__(self, comm: Communicator, grads: torch.Tensor, bounds: List[Tuple[int, int]],
-                 force: bool = False, transport: str | None = None):
+                 force: bool = False, transport: str | None = None, channels=None):
+        """channels: (channel bounds, channel indices per bucket) -- the buckets cut further
+        for the direct xGMI transport (ModelSpec.channel_bounds); default one per bucket."""
         self.comm = comm
         self.grads = grads
         self.out_grads = grads          # what the optimizer reads after finalize()
         self.bounds = list(bounds)
+        if channels is None:
+            channels = (list(self.bounds), [[i] for i in range(len(self.bounds))])
+        self.cbounds = list(channels[0])
+        self._bch = [list(c) for c in channels[1]]
         self.active = force or comm.world_size > 1
         self.grad_scale = 1.0 / comm.world_size
         self._native = None
@@ -74,7 +80,8 @@ class GradReducer:
         if grads.is_cuda and (transport == "xgmi" or
                               (transport == "auto" and isinstance(comm, RcclComm))):
             try:
-                x = XgmiTransport(comm, grads, self.bounds)
+                x = XgmiTransport(comm, grads, self.cbounds)
+                x.native.set_backward_channels(len(self._bch[0]))
             except Exception as e:           # mapping or self-check failed on some rank
                 if transport == "xgmi":
                     raise
@@ -112,7 +119,8 @@ class GradReducer:
         ``nch`` buckets (default: all; the others are exchanged in-launch by their producer,
         ``launch_optimizer(exchange=True)``); `wide`: the variant with twice the loads in
         flight, which fits only beside the small-band backward kernels."""
-        self._native.begin(nsteps, -1 if nch is None else int(nch), bool(wide))
+        n = -1 if nch is None else sum(len(self._bch[b]) for b in range(int(nch)))
+        self._native.begin(nsteps, n, bool(wide))
 
     def end(self) -> None:
         """Join the persistent collective back into the compute stream."""
@@ -124,20 +132,32 @@ class GradReducer:
                 return i
         raise ValueError(f"offset {offset} is in no bucket")
 
+    def channel_of(self, offset: int) -> int:
+        for i, (s, e) in enumerate(self.cbounds):
+            if s <= offset < e:
+                return i
+        raise ValueError(f"offset {offset} is in no channel")
+
+    def channels_of(self, bucket: int) -> list:
+        """The xGMI channels bucket `bucket` is cut into (one per bucket elsewhere)."""
+        return list(self._bch[bucket]) if self.kind == "xgmi" else [bucket]
+
     def waits_for(self, segments, exchanged=()) -> list:
-        """Flat (channel, multiplier) per optimizer segment: wait for that segment's bucket
-        (-1 for the buckets in `exchanged`, which the launch all-reduces itself)."""
+        """Flat (channel, multiplier) per optimizer segment: wait for the channel holding the
+        segment (-1 for the buckets in `exchanged`, which the launch all-reduces itself)."""
+        skip = {c for b in exchanged for c in self._bch[b]}
         out = []
         for sg in segments:
-            b = self.bucket_of(sg[0])
-            out += [-1, 0] if b in exchanged else [b, self._native.blocks(b)]
+            c = self.channel_of(sg[0])
+            out += [-1, 0] if c in skip else [c, self._native.blocks(c)]
         return out
 
     def bucket_ready(self, i: int) -> None:
         if not self.active:
             return
         if self._native is not None:
-            self._native.bucket_ready(i)
+            for c in self.channels_of(i):
+                self._native.bucket_ready(c)
             return
         s, e = self.bounds[i]
         view = self.grads[s:e]
@@ -161,7 +181,8 @@ class GradReducer:
         if not self.active:
             return
         if self._native is not None:
-            self._native.wait_bucket(i)
+            for c in self.channels_of(i):
+                self._native.wait_bucket(c)
             return
         w = self._pending.pop(i, None)
         if w is not None:

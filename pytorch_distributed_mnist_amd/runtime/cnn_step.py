@@ -406,6 +406,15 @@ class CnnStep(GpuStepBase):
         u = self._fc_update()
         return u[:16] + (self.wf1t,)
 
+    def _fc_carry_wait(self):
+        """xgmi streamed: the carried update waits for the channel of the fc1 weight, which the
+        optimizer no longer waits for (its own channel: models/specs.py channel_bounds)."""
+        red = self.reducer
+        if not red.streamed:
+            return None
+        ch = red.channel_of(self.arena.spec.offset("fc1.weight"))
+        return (red.sync, ch, int(red._native.blocks(ch)), float(red.timeout_s))
+
     def fwd_outputs(self, B: int):
         """cnn_fwd's training outputs for per-rank batch B: (xg, ylab, bands, a1g, xng) -- the
         band backward reads a1 + normalised x, the one-image backward the uint8 image."""
@@ -475,7 +484,8 @@ class CnnStep(GpuStepBase):
         C.cnn_fwd(self.ep_images.view(-1, 784), self.ep_labels, None, self.ctr[0:1], self.bfull, B,
                   P["conv1.weight"], P["conv1.bias"], self.w2, P["conv2.bias"], self.pool,
                   self.pmask, *self.fwd_outputs(B), spe=self.spe,
-                  fc_carry=self._fc_carry() if fwd_in else None)
+                  fc_carry=self._fc_carry() if fwd_in else None,
+                  fc_carry_wait=self._fc_carry_wait() if fwd_in else None)
         if carry_in and self.shard_fc:
             self.reducer.wait_gather()                # this step's W1 rows from every rank
             self.launch_optimizer(self._shard_segments()[1])
@@ -547,7 +557,7 @@ class CnnStep(GpuStepBase):
         if xgmi and red.streamed:
             # the optimizer publishes the conv bucket; its fc workgroups wait for bucket 0
             # (long reduced by now), its conv workgroups for bucket 1
-            self.launch_optimizer(signal_ch=1)
+            self.launch_optimizer(signal_ch=red.channels_of(1)[0])
             return
         if xgmi:
             if not early:

@@ -370,7 +370,8 @@ class GpuStepBase:
             # all-reduce their sums themselves; every other workgroup waits for its bucket
             # from the persistent collective (long done by now: it ran beside cnn_bwd)
             xg = dict(xg=red.sync, signal_ch=-1, waits=red.waits_for(segs, exchanged=(1,)),
-                      timeout_s=red.timeout_s, xchg=red._native, xchg_bucket=1)
+                      timeout_s=red.timeout_s, xchg=red._native,
+                      xchg_bucket=red.channels_of(1)[0])
         elif red.streamed:
             waits = red.waits_for(segs)
             if self.structure.xgmi_opt_wait:

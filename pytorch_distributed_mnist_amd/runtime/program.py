@@ -192,7 +192,8 @@ def build_local_program(arch: str, dtype: str, device, batch_size: int, train_sp
     opt = build_optimizer(optimizer, arena, SimpleNamespace(lr=lr, momentum=momentum,
                                                             weight_decay=weight_decay))
     comm = comm or LocalComm()
-    reducer = GradReducer(comm, arena.grads, spec.bucket_bounds(), force=force_comm,
+    reducer = GradReducer(comm, arena.grads, spec.bucket_bounds(), channels=spec.channel_bounds(),
+                          force=force_comm,
                           transport=transport)
     return TrainProgram(arch, dtype, arena, opt, reducer, train_split, test_split, batch_size,
                         use_graphs=use_graphs)

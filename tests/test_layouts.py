@@ -46,3 +46,18 @@ def test_cnn_bucket_sizes():
     assert spec.num_params == 1199882
     (s0, e0), (s1, e1) = spec.bucket_bounds()
     assert (e0 - s0) * 4 >= 4724264 and (e1 - s1) * 4 >= 75264
+
+
+def test_cnn_channel_bounds_give_fc1_weight_its_own_channel():
+    """The xGMI transport cuts the fc bucket at fc1.weight (models/specs.py channel_bounds):
+    the small fc parameters form channel 0, fc1.weight channel 1, the conv bucket channel 2;
+    every channel is 64-float aligned (the transport's requirement) and they tile the arena."""
+    spec = get_spec("cnn")
+    chans, of_bucket = spec.channel_bounds()
+    (s0, e0), (s1, e1) = spec.bucket_bounds()
+    off = spec.offset("fc1.weight")
+    assert chans == [(s0, off), (off, e0), (s1, e1)]
+    assert of_bucket == [[0, 1], [2]]
+    assert all(a % 64 == 0 and b % 64 == 0 for a, b in chans)
+    lin = get_spec("linear")
+    assert lin.channel_bounds() == (lin.bucket_bounds(), [[0]])
