@@ -1,10 +1,11 @@
 // The fc1-weight SGD update of the PREVIOUS step, run by extra workgroups of the forward
-// launch (world size > 1, "carried" update; runtime/cnn_step.py CnnStep._fwd_carry).
+// launch (world size > 1, "carried" update; runtime/cnn_step.py CnnStep._fwd_carry_on).
 //
 // At world size > 1 the fc1 update (4.7 MB of gradients, 28 MB of fp32 weight / momentum /
 // bf16-copy traffic) cannot run inside fc1_bwd as it does at world size 1: it needs the
 // all-reduced gradient.  In the optimizer launch it is bandwidth-bound work on the step's
-// critical path (the B = 32 optimizer: 7.7 us with it, ~3.5 without).  The next step's first
+// critical path (the B = 32 optimizer: 7.6 us with it, 5.2 without, RCCL nocarry;
+// profiles/r5/fc1_carry/).  The next step's first
 // kernel, the conv forward, does not read W1, and at the batches the forward is run at it
 // fills at most half of the chip's workgroup slots (two 512-thread workgroups per CU), so the
 // update's workgroups are appended to its grid and stream beside the conv workgroups; fc1_fwd
