@@ -58,7 +58,9 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     __shared__ int s_go;
     if (threadIdx.x == 0) {
       if (a.xg_signal_ch >= 0) xg_signal_ready(a.xg, a.xg_signal_ch);
-      s_go = s.wait_ch < 0 || xg_wait_done(a.xg, s.wait_ch, s.wait_mult, a.xg_timeout);
+      // no acquire: a waited segment reads its gradient with sc1 loads (gload below)
+      s_go = s.wait_ch < 0 || xg_wait_done(a.xg, s.wait_ch, s.wait_mult, a.xg_timeout,
+                                           /*acquire=*/false);
     }
     __syncthreads();
     if (!s_go) return;     // a peer never arrived: error bit set, the host raises
@@ -178,6 +180,21 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   }
 
   const Hyper h = make_hyper<KIND>(a);
+  // a segment that waited for its bucket (xgmi streamed) reads the gradient with sc1 loads,
+  // past this CU's L1, in place of an acquire after the wait: every byte of it was stored
+  // write-through and drained before the collective's workgroups added to DONE
+  // (MI355X_MICROARCH.md, the sc1 hand-off table)
+  const bool gsc1 = xgp != nullptr && s.wait_ch >= 0;
+  const __amdgpu_buffer_rsrc_t grs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), 0, 0x7fffffff, 0x00020000);
+  auto gload4 = [&](int64_t e) __attribute__((always_inline)) {
+    return gsc1 ? __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(grs, (int)(e * 4), 0, 16))
+                : *reinterpret_cast<const float4*>(G + e);
+  };
+  auto gload1 = [&](int64_t e) __attribute__((always_inline)) {
+    return gsc1 ? __hip_atomic_load(const_cast<float*>(G + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                : G[e];
+  };
   if (s.shadow_t == nullptr && !s.sfrag) {
     // plain segment: 8 contiguous floats per thread (2 x float4)
     const int64_t e0 = (int64_t)lb * CHUNK + threadIdx.x * 8;
@@ -186,7 +203,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       const int64_t e = e0 + q * 4;
       if (e + 4 <= numel) {
         float4 p = *reinterpret_cast<float4*>(P + e);
-        const float4 g = *reinterpret_cast<const float4*>(G + e);
+        const float4 g = gload4(e);
         float4 m = *reinterpret_cast<float4*>(M + e);
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (KIND == OPT_ADAM) v = *reinterpret_cast<float4*>(V + e);
@@ -209,7 +226,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       } else {
         for (int64_t j = e; j < numel && j < e + 4; ++j) {
           float m = M[j], v = (KIND == OPT_ADAM) ? V[j] : 0.f;
-          const float p = update<KIND>(P[j], G[j], m, v, h, a.grad_scale);
+          const float p = update<KIND>(P[j], gload1(j), m, v, h, a.grad_scale);
           P[j] = p;
           M[j] = m;
           if (KIND == OPT_ADAM) V[j] = v;
@@ -236,7 +253,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const float4 p4 = *reinterpret_cast<const float4*>(P + e + 4 * q);
-        const float4 g4 = *reinterpret_cast<const float4*>(G + e + 4 * q);
+        const float4 g4 = gload4(e + 4 * q);
         const float4 m4 = *reinterpret_cast<const float4*>(M + e + 4 * q);
         pv[4 * q] = p4.x; pv[4 * q + 1] = p4.y; pv[4 * q + 2] = p4.z; pv[4 * q + 3] = p4.w;
         gv[4 * q] = g4.x; gv[4 * q + 1] = g4.y; gv[4 * q + 2] = g4.z; gv[4 * q + 3] = g4.w;
@@ -270,7 +287,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
       for (int j = 0; j < 8 && col0 + j < s.cols; ++j) {
         const int64_t ej = e + j;
         float m = M[ej], v = (KIND == OPT_ADAM) ? V[ej] : 0.f;
-        const float p = update<KIND>(P[ej], G[ej], m, v, h, a.grad_scale);
+        const float p = update<KIND>(P[ej], gload1(ej), m, v, h, a.grad_scale);
         P[ej] = p;
         M[ej] = m;
         if (KIND == OPT_ADAM) V[ej] = v;
