@@ -69,7 +69,10 @@ constexpr int DW_MT = PDM_DW_MT;
 static_assert(DW_MT == 1 || DW_MT == 2, "dW tile: 64 or 128 hidden rows");
 constexpr int DW_FT = FEAT / 64;                      // 144 feature tiles
 constexpr int DW_TILES = DW_FT * (2 / DW_MT);         // 144 or 288
-constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
+#ifndef PDM_DWC
+#define PDM_DWC 128
+#endif
+constexpr int DWC = PDM_DWC;         // dW1 batch rows staged per LDS round
 constexpr int DX_COLS = 384;         // dX tile: 32 batch rows x 384 features per workgroup
 constexpr int DX_TILES = FEAT / DX_COLS;   // 24 = 8 XCDs x 3
 constexpr int DX_FT = DX_COLS / 64;        // 16-feature sub-tiles per wave (6)
