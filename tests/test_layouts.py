@@ -61,3 +61,18 @@ def test_cnn_channel_bounds_give_fc1_weight_its_own_channel():
     assert all(a % 64 == 0 and b % 64 == 0 for a, b in chans)
     lin = get_spec("linear")
     assert lin.channel_bounds() == (lin.bucket_bounds(), [[0]])
+
+
+def test_grad_reducer_channels_map_buckets():
+    """GradReducer keeps the bucket API (bucket_ready(i), wait_bucket(i)) over the xGMI
+    transport's finer channels; other transports have one channel per bucket."""
+    from pytorch_distributed_mnist_amd.parallel.comm import LocalComm
+    from pytorch_distributed_mnist_amd.parallel.reducer import GradReducer
+    spec = get_spec("cnn")
+    red = GradReducer(LocalComm(), torch.zeros(spec.total), spec.bucket_bounds(),
+                      channels=spec.channel_bounds())
+    assert red.cbounds == spec.channel_bounds()[0]
+    assert red.channels_of(0) == [0] and red.channels_of(1) == [1]      # not xgmi
+    assert red.channel_of(spec.offset("fc1.weight")) == 1
+    assert red.channel_of(spec.offset("fc2.bias")) == 0
+    assert red.channel_of(spec.offset("conv1.bias")) == 2
