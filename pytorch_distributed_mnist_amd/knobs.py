@@ -29,6 +29,8 @@ KNOBS: Dict[str, tuple] = {
     "PDM_SPLITK_CAP": ("32", "structure", "largest fc1_fwd split-K factor"),
     "PDM_FC1_CARRY_FWD": ("1", "structure", "0: world size > 1, the fc1 update in the optimizer "
                           "launch instead of the next step's forward launch"),
+    "PDM_FC1_CARRY_GRAPHS": ("1", "structure", "0: the carried fc1 update stops at every graph "
+                             "replay's last step instead of the train_steps call's"),
     "PDM_FUSE_HEAD": ("0", "structure", "1: fc1_fwd and the training head in one launch "
                       "(fc1_head; measured slower, profiles/r5/fc1_head/)"),
     "PDM_BANDS": (None, "structure", "row bands per image in the conv backward (1 = off)"),

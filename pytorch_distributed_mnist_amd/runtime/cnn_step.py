@@ -432,7 +432,11 @@ class CnnStep(GpuStepBase):
         # 4- and 8-row bands only (6 / 3 bands per image), not beside 12-row bands or cnn_bwd
         return self.bands(B) >= 3
 
-    def _train_seq(self, B: int, n: int, collective: bool = True) -> None:
+    def carries_across_graphs(self) -> bool:
+        return self._fwd_carry_on() and self.structure.fc1_carry_graphs
+
+    def _train_seq(self, B: int, n: int, collective: bool = True, cin: bool = False,
+                   cout: bool = False) -> None:
         # multi-GPU: each step leaves its fc-bucket update to the next one, whose cnn_fwd
         # runs while the fc gradients are still being all-reduced; the last step of the
         # sequence (a graph must rejoin the comm stream) does not carry
@@ -447,8 +451,10 @@ class CnnStep(GpuStepBase):
             # optimizer exchanges the conv bucket itself)
             self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
         for i in range(n):
+            # the fc1 update is carried across graph replays of one train_steps call too
+            # (cin / cout); only the call's last step updates in its own optimizer
             self._train_impl(B, carry_in=carry and i > 0, carry_out=carry and i < n - 1,
-                             fwd_in=fwd and i > 0, fwd_out=fwd and i < n - 1)
+                             fwd_in=fwd and (i > 0 or cin), fwd_out=fwd and (i < n - 1 or cout))
             self.phase = (self.phase + 1) % self.phase_period
         if streamed:
             self.reducer.end()

@@ -229,9 +229,15 @@ class GpuStepBase:
     GRAPH_STEPS = _GRAPH_STEPS
     GRAPH_SIZES = tuple(_GRAPH_STEPS >> i for i in range(_GRAPH_STEPS.bit_length()))
 
-    def _graph(self, B: int, nsteps: int, phase=None):
+    def carries_across_graphs(self) -> bool:
+        """Whether a step leaves work to the next one (CnnStep: the carried fc1 update), so
+        consecutive graph replays of one train_steps call hand it over: the graphs then come
+        in variants by (carry in, carry out)."""
+        return False
+
+    def _graph(self, B: int, nsteps: int, phase=None, cin: bool = False, cout: bool = False):
         phase = self.phase if phase is None else phase
-        key = (B, nsteps, phase)
+        key = (B, nsteps, phase, bool(cin), bool(cout))
         g = self.graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
@@ -247,7 +253,8 @@ class GpuStepBase:
                 with torch.cuda.graph(g):          # captured on a side stream
                     # the persistent collective stays out of the graph when it is launched
                     # per train_steps call (collective_outside): no cross-queue edges
-                    self._train_seq(B, nsteps, collective=not self.collective_outside())
+                    self._train_seq(B, nsteps, collective=not self.collective_outside(),
+                                    cin=cin, cout=cout)
             finally:
                 if gc_on:
                     gc.enable()
@@ -255,9 +262,15 @@ class GpuStepBase:
             self.graphs[key] = g
         return g
 
-    def _replay(self, B: int, nsteps: int) -> None:
-        self._graph(B, nsteps).replay()
+    def _replay(self, B: int, nsteps: int, cin: bool = False, cout: bool = False) -> None:
+        self._graph(B, nsteps, cin=cin, cout=cout).replay()
         self.phase = (self.phase + nsteps) % self.phase_period
+
+    def _carry_flags(self, nreplays: int):
+        """(carry in, carry out) of each of `nreplays` consecutive replays of one call."""
+        if not self.carries_across_graphs():
+            return [(False, False)] * nreplays
+        return [(i > 0, i < nreplays - 1) for i in range(nreplays)]
 
     def prepare(self, B: int, sizes=None) -> None:
         """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, or
@@ -266,9 +279,11 @@ class GpuStepBase:
         when replayed."""
         if not self.use_graphs:
             return
-        for n, ph in ((n, ph) for n in (sizes or self.GRAPH_SIZES)
-                      for ph in range(self.phase_period)):
-            g = self._graph(B, n, ph)
+        flags = ((False, False), (False, True), (True, True), (True, False)) \
+            if self.carries_across_graphs() else ((False, False),)
+        for n, ph, (ci, co) in ((n, ph, f) for n in (sizes or self.GRAPH_SIZES)
+                                for ph in range(self.phase_period) for f in flags):
+            g = self._graph(B, n, ph, ci, co)
             try:
                 exe = g.raw_cuda_graph_exec()
             except (AttributeError, RuntimeError):
@@ -286,6 +301,7 @@ class GpuStepBase:
             k = self.GRAPH_STEPS
             r = n % k
             sizes = [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]
+            flags = self._carry_flags(len(sizes))
             if self.collective_outside():
                 # one persistent collective for all n steps, launched eagerly on its own
                 # stream beside the graph replays: the steps hand it their buckets through
@@ -295,13 +311,13 @@ class GpuStepBase:
                 # capture synchronizes the device, which would wait for a running
                 # collective that waits for steps not yet launched.
                 ph = self.phase
-                for size in sizes:
-                    self._graph(B, size, ph)
+                for size, (ci, co) in zip(sizes, flags):
+                    self._graph(B, size, ph, ci, co)
                     ph = (ph + size) % self.phase_period
                 self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
-            for size in sizes:
+            for size, (ci, co) in zip(sizes, flags):
                 self._issue_ahead()
-                self._replay(B, size)
+                self._replay(B, size, ci, co)
                 self._ctr_host += size
         else:
             self._issue_ahead()
@@ -328,9 +344,11 @@ class GpuStepBase:
         """Whether the wide persistent collective fits beside this step's kernels at B."""
         return False
 
-    def _train_seq(self, B: int, n: int, collective: bool = True) -> None:
+    def _train_seq(self, B: int, n: int, collective: bool = True, cin: bool = False,
+                   cout: bool = False) -> None:
         """n consecutive steps (captured together into one graph, or eager); `collective`:
-        launch (and join) the persistent collective for them here."""
+        launch (and join) the persistent collective for them here; cin / cout: work carried
+        in from the previous sequence / out to the next (carries_across_graphs)."""
         streamed = self.reducer.streamed and collective
         if streamed:
             # one launch for the n steps

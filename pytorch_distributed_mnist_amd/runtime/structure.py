@@ -27,6 +27,9 @@ class StepStructure:
     # update runs in extra workgroups of step k+1's forward launch instead of the optimizer
     # (kernels/fc_carry.h); the last step of a sequence updates in its own optimizer
     fc1_carry_fwd: bool = True
+    # ... also from one graph replay to the next within a train_steps call (graph variants by
+    # carry in / out), so only the call's last step updates fc1 in its optimizer
+    fc1_carry_graphs: bool = True
     # training: fc1_fwd and the head in one launch (fc1_head) where the grid allows it.  Off:
     # measured slower than the two launches (B = 256: 60.1-61.2 vs 53.1-53.7 us per step;
     # B = 32: 38.9 vs 37.4-37.7; profiles/r5/fc1_head/) -- the write-through partials and
@@ -89,6 +92,7 @@ class StepStructure:
                    splitk_cap=int(knobs.get("PDM_SPLITK_CAP", str(d.splitk_cap))),
                    fuse_head=flag("PDM_FUSE_HEAD", d.fuse_head),
                    fc1_carry_fwd=flag("PDM_FC1_CARRY_FWD", d.fc1_carry_fwd),
+                   fc1_carry_graphs=flag("PDM_FC1_CARRY_GRAPHS", d.fc1_carry_graphs),
                    fuse_conv_reduce=flag("PDM_FUSE_CONV_REDUCE", d.fuse_conv_reduce),
                    fuse_fc1=flag("PDM_FUSE_FC1", d.fuse_fc1),
                    fc1_wt_double=flag("PDM_FC1_WT2", d.fc1_wt_double),
