@@ -31,6 +31,9 @@ KNOBS: Dict[str, tuple] = {
                           "launch instead of the next step's forward launch"),
     "PDM_FC1_CARRY_GRAPHS": ("1", "structure", "0: the carried fc1 update stops at every graph "
                              "replay's last step instead of the train_steps call's"),
+    "PDM_FC1_CARRY_LOCAL": ("1", "structure", "0: world size 1 fuses the fc1 update into "
+                            "fc1_bwd at every batch instead of carrying it into the next "
+                            "forward launch where that is faster (B > 128)"),
     "PDM_FUSE_HEAD": ("0", "structure", "1: fc1_fwd and the training head in one launch "
                       "(fc1_head; measured slower, profiles/r5/fc1_head/)"),
     "PDM_BANDS": (None, "structure", "row bands per image in the conv backward (1 = off)"),
@@ -85,6 +88,8 @@ KNOBS: Dict[str, tuple] = {
     "PDM_XG_DIAG": (None, "build", "1: xgmi flag protocol without payload (timing only)"),
     "PDM_FC1BWD_WPE": (None, "build", "fc1_bwd minimum waves per SIMD (launch bounds)"),
     "PDM_DWC": (None, "build", "fc1_bwd weight-gradient batch rows per LDS round"),
+    "PDM_FCC_FIRST": (None, "build", "1: the carried fc1 update's workgroups first in cnn_fwd's "
+                      "grid (experiment)"),
     "PDM_DG_MTP": (None, "build", "cnn_bwd dgrad tiles per pass"),
     "PDM_DG_PFD": (None, "build", "cnn_bwd dgrad prefetch distance"),
     "PDM_HIPCC_FLAGS": (None, "build", "extra hipcc flags"),

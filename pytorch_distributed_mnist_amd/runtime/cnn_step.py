@@ -169,6 +169,8 @@ class CnnStep(GpuStepBase):
         # tiles (the gradient is still in registers; those tiles have slack next to the dX
         # tiles of the same launch); the optimizer launch then only re-derives the transposed
         # bf16 copy W1^T from the updated W1 (PDM_FUSE_FC1=0 disables)
+        # (at the batches where fc1_carry_local hands it to the next forward launch instead,
+        # _local_carry, fc1_bwd stores the gradient and does not update)
         self.fuse_fc1 = self.fuse_conv_reduce and self.opt.kind == "sgd" and st.fuse_fc1
         # ... and writes W1^T too, double-buffered by step parity (this step's dX tiles read
         # one half while its weight tiles write the other), so the optimizer launch skips fc1
@@ -364,14 +366,15 @@ class CnnStep(GpuStepBase):
             fc1_off = self.arena.spec.offset("fc1.weight")
             for sg in self._opt_segments:
                 name = by_off.get(sg[0])
+                if name is None and skip_fc1 and sg[0] == fc1_off:
+                    continue
                 if name is None and self.fuse_fc1 and sg[0] == fc1_off:
                     # updated by fc1_bwd: only W1^T = transpose(W1) is left to write, unless
                     # fc1_bwd writes it too (double-buffered)
                     if not self.wt_double:
                         plain.append((sg[0], sg[1], sg[2], sg[3], sg[4], None, True, True, True))
                 elif name is None:
-                    if not (skip_fc1 and sg[0] == fc1_off):
-                        plain.append(sg)
+                    plain.append(sg)
                 else:
                     sg = tuple(sg) + (None,) * (9 - len(sg))
                     slab_segs.append(sg[:5] + ((self.conv_slab, nblk, col[name], C.CNN_CONV_SLAB),) +
@@ -388,12 +391,26 @@ class CnnStep(GpuStepBase):
         off = self.arena.spec.offset("fc1.weight")
         return [sg for sg in self._opt_segments if sg[0] != off]
 
-    def _fwd_carry_on(self) -> bool:
-        """World size > 1, SGD: step k's fc1 update runs in step k+1's forward launch
-        (kernels/fc_carry.h) -- on the xgmi in-launch-exchange step and the RCCL nocarry step."""
+    def _local_carry(self, B: int) -> bool:
+        """World size 1, SGD, fc1_carry_local: the fc1 update of a batch-B step runs in the
+        next forward launch instead of fc1_bwd's weight tiles -- at the batches whose forward
+        is the one-image cnn_fwd (its grid leaves room for the update's workgroups: B = 256
+        53.2 vs 53.9 us per step); the band forward of B <= 128 pays more for them than fc1_bwd
+        saves (B = 32: 38.6 vs 37.3; profiles/r5/fc1_carry_local/).  The last step of a
+        train_steps call keeps the fused update."""
+        st = self.structure
+        return (not self.reducer.active and self.fuse_fc1 and st.fc1_carry_fwd and
+                st.fc1_carry_local and self.bands(B) == 1 and
+                choose_fwd_bands(B, st.fwd_bands, st.bands) == 1)
+
+    def _fwd_carry_on(self, B: int) -> bool:
+        """SGD: step k's fc1 update runs in step k+1's forward launch (kernels/fc_carry.h) --
+        at world size > 1 on the xgmi in-launch-exchange step and the RCCL nocarry step; at
+        world size 1 where _local_carry says so."""
         red = self.reducer
-        if not (red.active and self.structure.fc1_carry_fwd and self.opt.kind == "sgd") or \
-                self.shard_fc:
+        if not red.active:
+            return self._local_carry(B)
+        if not (self.structure.fc1_carry_fwd and self.opt.kind == "sgd") or self.shard_fc:
             return False
         if self._xchg():
             return True
@@ -404,7 +421,7 @@ class CnnStep(GpuStepBase):
         """The carried fc1 update (cnn_fwd fc_carry): the fused update's arguments, reading the
         all-reduced gradient, writing the single W1^T copy."""
         u = self._fc_update()
-        return u[:16] + (self.wf1t,)
+        return u[:16] + (self.current_wf1t(),)
 
     def _fc_carry_wait(self):
         """xgmi streamed: the carried update waits for the channel of the fc1 weight, which the
@@ -432,8 +449,8 @@ class CnnStep(GpuStepBase):
         # 4- and 8-row bands only (6 / 3 bands per image), not beside 12-row bands or cnn_bwd
         return self.bands(B) >= 3
 
-    def carries_across_graphs(self) -> bool:
-        return self._fwd_carry_on() and self.structure.fc1_carry_graphs
+    def carries_across_graphs(self, B: int) -> bool:
+        return self._fwd_carry_on(B) and self.structure.fc1_carry_graphs
 
     def _train_seq(self, B: int, n: int, collective: bool = True, cin: bool = False,
                    cout: bool = False) -> None:
@@ -444,7 +461,7 @@ class CnnStep(GpuStepBase):
         # sharded: the W1 all-gather and the W1^T transpose are carried past the next cnn_fwd
         carry = rccl and (self.shard_fc or (self.fc_carry and not self.fc_early))
         # world size > 1, SGD: each step's fc1 update runs in the next step's forward launch
-        fwd = self._fwd_carry_on()
+        fwd = self._fwd_carry_on(B)
         streamed = self.reducer.streamed and collective
         if streamed:
             # one persistent xgmi collective for the n steps (the fc bucket only when the
@@ -513,7 +530,8 @@ class CnnStep(GpuStepBase):
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.current_wf1t(), B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view(),
-                  self._fc_update() if self.fuse_fc1 and self.fuse_conv_reduce else None)
+                  # (world size 1: fused unless the next forward carries it, _local_carry)
+                  self._fc_update() if self.fuse_fc1 and not fwd_out else None)
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
         rccl_early = (self.fc_early and not xgmi and red.active and
                       getattr(red, "_native", None) is not None)
@@ -534,7 +552,7 @@ class CnnStep(GpuStepBase):
                   ipb, self.conv_slab, xs, bands, self.a1g, self.xng)
         if self.fuse_conv_reduce:
             # world_size 1: no all-reduce, the conv slab reduction runs inside the update
-            self.launch_optimizer(self._fused_segments(nblk))
+            self.launch_optimizer(self._fused_segments(nblk, skip_fc1=fwd_out))
             return
         if self._xchg():
             # xgmi streamed: the optimizer reduces the conv slabs AND all-reduces the conv

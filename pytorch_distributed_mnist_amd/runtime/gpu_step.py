@@ -229,8 +229,8 @@ class GpuStepBase:
     GRAPH_STEPS = _GRAPH_STEPS
     GRAPH_SIZES = tuple(_GRAPH_STEPS >> i for i in range(_GRAPH_STEPS.bit_length()))
 
-    def carries_across_graphs(self) -> bool:
-        """Whether a step leaves work to the next one (CnnStep: the carried fc1 update), so
+    def carries_across_graphs(self, B: int) -> bool:
+        """Whether a step of batch B leaves work to the next one (CnnStep: the carried fc1 update), so
         consecutive graph replays of one train_steps call hand it over: the graphs then come
         in variants by (carry in, carry out)."""
         return False
@@ -266,9 +266,9 @@ class GpuStepBase:
         self._graph(B, nsteps, cin=cin, cout=cout).replay()
         self.phase = (self.phase + nsteps) % self.phase_period
 
-    def _carry_flags(self, nreplays: int):
+    def _carry_flags(self, B: int, nreplays: int):
         """(carry in, carry out) of each of `nreplays` consecutive replays of one call."""
-        if not self.carries_across_graphs():
+        if not self.carries_across_graphs(B):
             return [(False, False)] * nreplays
         return [(i > 0, i < nreplays - 1) for i in range(nreplays)]
 
@@ -280,7 +280,7 @@ class GpuStepBase:
         if not self.use_graphs:
             return
         flags = ((False, False), (False, True), (True, True), (True, False)) \
-            if self.carries_across_graphs() else ((False, False),)
+            if self.carries_across_graphs(B) else ((False, False),)
         for n, ph, (ci, co) in ((n, ph, f) for n in (sizes or self.GRAPH_SIZES)
                                 for ph in range(self.phase_period) for f in flags):
             g = self._graph(B, n, ph, ci, co)
@@ -301,7 +301,7 @@ class GpuStepBase:
             k = self.GRAPH_STEPS
             r = n % k
             sizes = [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]
-            flags = self._carry_flags(len(sizes))
+            flags = self._carry_flags(B, len(sizes))
             if self.collective_outside():
                 # one persistent collective for all n steps, launched eagerly on its own
                 # stream beside the graph replays: the steps hand it their buckets through

@@ -30,6 +30,10 @@ class StepStructure:
     # ... also from one graph replay to the next within a train_steps call (graph variants by
     # carry in / out), so only the call's last step updates fc1 in its optimizer
     fc1_carry_graphs: bool = True
+    # world size 1, SGD: carry the fc1 update into the next forward launch there too, instead
+    # of fusing it into fc1_bwd's weight-gradient tiles, at the batches CnnStep._local_carry
+    # names (fc1_bwd then stores the gradient; a call's last step still fuses its update)
+    fc1_carry_local: bool = True
     # training: fc1_fwd and the head in one launch (fc1_head) where the grid allows it.  Off:
     # measured slower than the two launches (B = 256: 60.1-61.2 vs 53.1-53.7 us per step;
     # B = 32: 38.9 vs 37.4-37.7; profiles/r5/fc1_head/) -- the write-through partials and
@@ -93,6 +97,7 @@ class StepStructure:
                    fuse_head=flag("PDM_FUSE_HEAD", d.fuse_head),
                    fc1_carry_fwd=flag("PDM_FC1_CARRY_FWD", d.fc1_carry_fwd),
                    fc1_carry_graphs=flag("PDM_FC1_CARRY_GRAPHS", d.fc1_carry_graphs),
+                   fc1_carry_local=flag("PDM_FC1_CARRY_LOCAL", d.fc1_carry_local),
                    fuse_conv_reduce=flag("PDM_FUSE_CONV_REDUCE", d.fuse_conv_reduce),
                    fuse_fc1=flag("PDM_FUSE_FC1", d.fuse_fc1),
                    fc1_wt_double=flag("PDM_FC1_WT2", d.fc1_wt_double),

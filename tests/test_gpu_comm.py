@@ -128,7 +128,7 @@ def test_fc1_update_carried_into_forward_is_bit_identical(gpu, transport, B):
             p.gpu.set_rccl_mode("nocarry")
         p.gpu.structure = p.gpu.structure.with_(fc1_carry_fwd=carry)
         p.gpu.invalidate_graphs()
-        assert p.gpu._fwd_carry_on() == carry
+        assert p.gpu._fwd_carry_on(B) == carry
         p.optimizer.sync_hyperparams()
         p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
         p.train_epoch()
@@ -139,6 +139,36 @@ def test_fc1_update_carried_into_forward_is_bit_identical(gpu, transport, B):
                     p.gpu.wf1t.clone()))
         p.reducer.close()
         comm.close()
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [160, 256])
+def test_fc1_update_carried_at_world_size_1_is_bit_identical(gpu, B, monkeypatch):
+    """World size 1 with fc1_carry_local: fc1_bwd stores the fc1-weight gradient and the next
+    forward launch updates from it, instead of the update fused into fc1_bwd's weight tiles.
+    Same update, same bits: weights, momentum, W1 and the W1^T the next fc1_bwd reads, over
+    two epochs of 8-step graphs, a sequence of one and a (banded, fused) ragged tail."""
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.runtime.program import build_local_program
+    train = synthetic_split(B * 9 + 40, True)
+    test = synthetic_split(256, False)
+    out = []
+    for carry in ("0", "1"):
+        monkeypatch.setenv("PDM_FC1_CARRY_LOCAL", carry)
+        p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.05,
+                                momentum=0.9, seed=4, use_graphs=True)
+        assert p.gpu._fwd_carry_on(B) == (carry == "1")
+        assert not p.gpu._fwd_carry_on(40)
+        p.optimizer.sync_hyperparams()
+        for epoch in range(2):
+            p.set_train_indices(distributed_indices(len(train), 1, 0, epoch))
+            p.train_epoch()
+        torch.cuda.synchronize()
+        o = p.optimizer
+        out.append((p.arena.params.clone(), o.momentum_buffer.clone(), p.gpu.wf1.clone(),
+                    p.gpu.current_wf1t().clone()))
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
 
