@@ -63,30 +63,18 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
     uint8_t* __restrict__ xg, int32_t* __restrict__ ylab, const FcUpdate fcc, int nconv) {
   __shared__ __attribute__((aligned(16))) char smem[F_TOTAL];
   static_assert(F_TOTAL >= FCC_LDS + 4, "carried fc1 update tiles fit the forward's LDS");
-#if PDM_FCC_FIRST
-  // experiment: the update's workgroups first in the grid (dispatched ahead of the conv ones)
-  const int ncar = (int)gridDim.x - nconv;
-  if constexpr (CARRY) {
-    if ((int)blockIdx.x < ncar) {
-      fc_carry_role(fcc, blockIdx.x, ncar, smem);
-      return;
-    }
-  }
-  const int img = (int)blockIdx.x - ncar;
-#else
   if constexpr (CARRY) {
     if ((int)blockIdx.x >= nconv) {
       fc_carry_role(fcc, blockIdx.x - nconv, gridDim.x - nconv, smem);
       return;
     }
   }
-  const int img = blockIdx.x;
-#endif
   bf16x4* x3 = reinterpret_cast<bf16x4*>(smem + F_X3);
   char* a1s = smem + F_A1;
   bf16* ps = reinterpret_cast<bf16*>(smem + F_PS);
   uint8_t* ms = reinterpret_cast<uint8_t*>(smem + F_MS);
 
+  const int img = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;

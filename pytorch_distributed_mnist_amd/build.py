@@ -71,7 +71,7 @@ def compile_flags(abi: int, inc):
     if knobs.get("PDM_DIAG_ROLES"):                   # fc1_bwd single-role launches
         flags.append("-DPDM_DIAG_ROLES=1")
     for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS", "PDM_NT", "PDM_WT",
-              "PDM_XG_WG", "PDM_XG_DIAG", "PDM_FC1BWD_WPE", "PDM_DWC", "PDM_FCC_FIRST"):   # tuning experiments (diagnostic builds)
+              "PDM_XG_WG", "PDM_XG_DIAG", "PDM_FC1BWD_WPE", "PDM_DWC"):   # tuning experiments (diagnostic builds)
         if os.environ.get(k):
             flags.append(f"-D{k}={int(os.environ[k])}")
     if knobs.get("PDM_HIPCC_FLAGS"):                  # compiler experiments (diagnostic builds)

@@ -88,8 +88,6 @@ KNOBS: Dict[str, tuple] = {
     "PDM_XG_DIAG": (None, "build", "1: xgmi flag protocol without payload (timing only)"),
     "PDM_FC1BWD_WPE": (None, "build", "fc1_bwd minimum waves per SIMD (launch bounds)"),
     "PDM_DWC": (None, "build", "fc1_bwd weight-gradient batch rows per LDS round"),
-    "PDM_FCC_FIRST": (None, "build", "1: the carried fc1 update's workgroups first in cnn_fwd's "
-                      "grid (experiment)"),
     "PDM_DG_MTP": (None, "build", "cnn_bwd dgrad tiles per pass"),
     "PDM_DG_PFD": (None, "build", "cnn_bwd dgrad prefetch distance"),
     "PDM_HIPCC_FLAGS": (None, "build", "extra hipcc flags"),
