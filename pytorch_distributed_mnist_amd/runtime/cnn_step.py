@@ -419,7 +419,7 @@ class CnnStep(GpuStepBase):
 
     def _fc_carry(self):
         """The carried fc1 update (cnn_fwd fc_carry): the fused update's arguments, reading the
-        all-reduced gradient, writing the single W1^T copy."""
+        (all-reduced) gradient, writing the W1^T copy this step's fc1_bwd reads."""
         u = self._fc_update()
         return u[:16] + (self.current_wf1t(),)
 
@@ -460,7 +460,8 @@ class CnnStep(GpuStepBase):
         rccl = self.reducer.active and getattr(self.reducer, "kind", None) == "rccl"
         # sharded: the W1 all-gather and the W1^T transpose are carried past the next cnn_fwd
         carry = rccl and (self.shard_fc or (self.fc_carry and not self.fc_early))
-        # world size > 1, SGD: each step's fc1 update runs in the next step's forward launch
+        # SGD (world size > 1; world size 1 at B > 128): each step's fc1 update runs in the
+        # next step's forward launch
         fwd = self._fwd_carry_on(B)
         streamed = self.reducer.streamed and collective
         if streamed:
