@@ -22,7 +22,14 @@ namespace cnn {
 
 constexpr int FCC_TR = 32, FCC_TC = 64;
 constexpr int FCC_TILES = (HID / FCC_TR) * (FEAT / FCC_TC);   // 576
-constexpr int FCC_LDS = 2 * FCC_TC * (FCC_TR + 8) * 2;         // two transpose tiles: 10 KB
+// two transpose tiles of [FCC_TC][FCC_TR] bf16 (8 KB); the 16-B chunk k of row c is stored
+// at chunk k ^ ((c >> 3) & 3): the column-wise 2-B writes of a wave (8 rows, 8 apart) spread
+// over 4 chunk positions instead of one bank group, 2-way instead of 8-way, and the row-wise
+// 16-B reads are conflict-free (tools/lds_bank_model.py; the padded layout: 8-way / 3-way)
+constexpr int FCC_LDS = 2 * FCC_TC * FCC_TR * 2;
+__device__ __forceinline__ int fcc_tpos(int c, int col) {
+  return c * FCC_TR + ((((col >> 3) ^ (c >> 3)) & 3) << 3) + (col & 7);
+}
 // update workgroups, two pairs of tiles each (288 workgroups of one pair were slower at
 // B = 32, where they would still fit one round beside the band workgroups:
 // profiles/r5/fc1_carry/)
@@ -45,8 +52,7 @@ __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg
   const __amdgpu_buffer_rsrc_t grs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(u.g), 0, 0x7fffffff, 0x00020000);
   const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
-  bf16 (*tile)[FCC_TR + 8] =
-      reinterpret_cast<bf16 (*)[FCC_TR + 8]>(smem + half * FCC_TC * (FCC_TR + 8) * 2);
+  bf16* tile = reinterpret_cast<bf16*>(smem + half * FCC_TC * FCC_TR * 2);
   const optim_detail::Hyper h = optim_detail::make_hyper<OPT_SGD>(u, *u.lr, *u.step);
   constexpr int tiles_c = FEAT / FCC_TC;
   const int r = t >> 3, c8 = (t & 7) * 8;
@@ -76,7 +82,7 @@ __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg
         float v = 0.f;
         pv[j] = optim_detail::update<OPT_SGD>(pv[j], gv[j], mv[j], v, h, u.grad_scale);
         hb[j] = to_bf16(pv[j]);
-        tile[c8 + j][r] = hb[j];
+        tile[fcc_tpos(c8 + j, r)] = hb[j];
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -92,7 +98,7 @@ __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg
       // transposed store: thread -> (col c, 8 consecutive rows) = one 16-B store
       const int c = t >> 2, rr = (t & 3) * 8;
       *reinterpret_cast<bf16x8*>(u.shadow_t_next + shadow_t_pos(1, HID, tr0 + rr, tc0 + c)) =
-          *reinterpret_cast<const bf16x8*>(&tile[c][rr]);
+          *reinterpret_cast<const bf16x8*>(&tile[fcc_tpos(c, rr)]);
     }
     __syncthreads();
   }
