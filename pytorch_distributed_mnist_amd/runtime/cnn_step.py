@@ -531,8 +531,12 @@ class CnnStep(GpuStepBase):
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.current_wf1t(), B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view(),
-                  # (world size 1: fused unless the next forward carries it, _local_carry)
-                  self._fc_update() if self.fuse_fc1 and not fwd_out else None)
+                  # (world size 1: fused unless the next forward carries it, _local_carry;
+                  # when this program's full batches carry it, and so store the fc1 gradient,
+                  # every fused step -- a call's last, the ragged tail -- stores it too, so the
+                  # gradient arena never holds an older step's gradient)
+                  self._fc_update(store_grad=self._local_carry(self.bfull))
+                  if self.fuse_fc1 and not fwd_out else None)
         xgmi = getattr(self.reducer, "kind", None) == "xgmi"
         rccl_early = (self.fc_early and not xgmi and red.active and
                       getattr(red, "_native", None) is not None)
@@ -649,8 +653,9 @@ class CnnStep(GpuStepBase):
         return (red.active and getattr(red, "kind", None) == "xgmi" and red.streamed and
                 self.structure.xgmi_exchange)
 
-    def _fc_update(self):
-        """fc1_bwd's fused fc1-weight SGD update (bind.cpp make_fc_update)."""
+    def _fc_update(self, store_grad: bool = False):
+        """fc1_bwd's fused fc1-weight SGD update (bind.cpp make_fc_update); store_grad: store
+        the gradient it consumes even without keep_grads."""
         o = self.opt
         g = o.param_groups[0]
         off = self.arena.spec.offset("fc1.weight")
@@ -659,7 +664,8 @@ class CnnStep(GpuStepBase):
                 o.momentum_buffer[off:off + n], None, self.wf1, o._lr_dev, o._step_dev, 0.0, 0.0,
                 0.0, float(g["weight_decay"]), float(g["momentum"]), float(g["dampening"]),
                 bool(g["nesterov"]), float(self.reducer.grad_scale),
-                self.wf1t2[1 - self.phase] if self._wt_double_on() else None, self.keep_grads)
+                self.wf1t2[1 - self.phase] if self._wt_double_on() else None,
+                self.keep_grads or store_grad)
 
     def _wt_double_on(self) -> bool:
         return self.fuse_fc1 and self.fuse_conv_reduce and self.wt_double
@@ -684,9 +690,10 @@ class CnnStep(GpuStepBase):
 
     def _poison_unkept_grads(self) -> None:
         """With the fused fc1 update and keep_grads off, fc1_bwd consumes the fc1-weight
-        gradient in registers and never stores it: fill that slice of the gradient arena with
-        NaN so a later reader (norm logging, clipping, dumps) fails visibly instead of seeing
-        a stale step's values."""
+        gradient in registers and never stores it (but at the batches where the update is
+        carried, _local_carry): fill that slice of the gradient arena with NaN so a later
+        reader (norm logging, clipping, dumps) fails visibly instead of seeing a stale step's
+        values."""
         if self.fuse_fc1 and self.fuse_conv_reduce and not self.keep_grads:
             self.G["fc1.weight"].fill_(float("nan"))
 

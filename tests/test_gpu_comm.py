@@ -173,6 +173,32 @@ def test_fc1_update_carried_at_world_size_1_is_bit_identical(gpu, B, monkeypatch
         assert torch.equal(a, b)
 
 
+def test_fc1_grad_arena_is_current_with_carried_updates(gpu, monkeypatch):
+    """World size 1, B = 256: the carried steps store the fc1-weight gradient, so the fused
+    steps (a call's last step, the ragged tail) store theirs too -- after an epoch the arena
+    holds the tail step's gradient, as with PDM_KEEP_GRADS=1, not an older step's."""
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.runtime.program import build_local_program
+    B = 256
+    train = synthetic_split(B * 9 + 40, True)
+    test = synthetic_split(256, False)
+    out = []
+    for keep in ("0", "1"):
+        monkeypatch.setenv("PDM_KEEP_GRADS", keep)
+        p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.05,
+                                momentum=0.9, seed=4, use_graphs=True)
+        assert p.gpu._fwd_carry_on(B) and p.gpu.keep_grads == (keep == "1")
+        p.optimizer.sync_hyperparams()
+        p.set_train_indices(distributed_indices(len(train), 1, 0, 0))
+        p.train_epoch()
+        torch.cuda.synchronize()
+        out.append((p.gpu.G["fc1.weight"].clone(), p.arena.params.clone()))
+    assert torch.isfinite(out[0][0]).all()
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def test_rccl_comm_count(gpu):
     comm = _comm(gpu)
     assert comm.comm_count() == 1
