@@ -27,8 +27,9 @@ KNOBS: Dict[str, tuple] = {
     "PDM_FC1_WT2": ("1", "structure", "0: the optimizer re-derives W1^T (no double buffer)"),
     "PDM_KEEP_GRADS": ("0", "diag", "1: store the fc1 weight gradient the fused update consumes"),
     "PDM_SPLITK_CAP": ("32", "structure", "largest fc1_fwd split-K factor"),
-    "PDM_FC1_CARRY_FWD": ("1", "structure", "0: world size > 1, the fc1 update in the optimizer "
-                          "launch instead of the next step's forward launch"),
+    "PDM_FC1_CARRY_FWD": ("1", "structure", "0: the fc1 update never carried into the next "
+                          "step's forward launch (world size > 1: in the optimizer launch; "
+                          "world size 1: fused into fc1_bwd)"),
     "PDM_FC1_CARRY_GRAPHS": ("1", "structure", "0: the carried fc1 update stops at every graph "
                              "replay's last step instead of the train_steps call's"),
     "PDM_FC1_CARRY_LOCAL": ("1", "structure", "0: world size 1 fuses the fc1 update into "
