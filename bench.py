@@ -74,24 +74,47 @@ def parse(argv=None):
 RCCL_MODES = ("carry", "nocarry", "side", "early", "zero")
 
 
-def step_candidates(reducers: dict, model: str, shard_ok) -> list:
-    """Candidate step structures [(name, reducer, structure)]: every transport, and for RCCL
-    the fc-update placement (cnn_step.CnnStep: carry = carried past the next cnn_fwd,
-    nocarry = one grouped launch, side = on a side stream, early = all-reduce issued during
-    the conv backward).  PDM_RCCL_MODE forces one.  'zero' (the fc1 update sharded over the
-    ranks) is a candidate only when forced: its multi-rank RCCL path has not run on hardware
-    yet, so the automatic choice never lands on it."""
+def step_candidates(reducers: dict, model: str, B: int, shard_ok, exchange_step: bool = True) -> list:
+    """Candidate step structures [(name, reducer, rccl mode, xgmi in-launch exchange)] for
+    per-rank batch B: at most four, each kept for what it can win on a real N-GPU node,
+    where the 4.7 MB fc bucket's all-reduce takes tens of microseconds on the wire:
+
+      xgmi          direct xGMI transport, streamed: the fc bucket travels beside the conv
+                    backward and fc1.weight's update waits for it only in the next forward;
+                    the conv bucket is exchanged inside the optimizer launch (fewest launches)
+      xgmi-noxchg   the same with the conv bucket through conv_reduce + the persistent
+                    collective: the fallback when the in-launch exchange fails on real peers
+      rccl-nocarry  one grouped RCCL launch for both buckets, the fc1 update carried into the
+                    next forward: the fastest RCCL structure in every N = 1 calibration
+                    (profiles/r5/final4/bench.jsonl)
+      rccl          (B >= 256) carry: the fc all-reduce overlaps the conv update and the next
+                    cnn_fwd; at B = 256 cnn_bwd fills every CU, so RCCL's kernel (19.7 KB LDS)
+                    cannot start before it ends and 'early' gains nothing
+      rccl-early    (B < 256) the fc all-reduce issued during the conv backward, whose band
+                    kernels leave CUs free for RCCL's kernel (DDP's overlap in backward)
+
+    'side' (20 us slower at every N = 1 point) and 'zero' (the sharded fc1 update) run only
+    when PDM_RCCL_MODE forces them.  PDM_RCCL_MODE forces one RCCL mode."""
     forced = knobs.get("PDM_RCCL_MODE")
     if forced is not None and forced not in RCCL_MODES:
         raise SystemExit(f"PDM_RCCL_MODE={forced!r}: choose from {RCCL_MODES}")
     cands = []
     for name, red in reducers.items():
         if name == "rccl" and model == "cnn":
-            ok = [m for m in RCCL_MODES if m != "zero" or (forced == "zero" and shard_ok(red))]
-            for m in ([forced] if forced in ok else ok):
-                cands.append(("rccl" if m == "carry" else f"rccl-{m}", red, m))
+            if forced is not None:
+                if forced == "zero" and not shard_ok(red):
+                    continue
+                modes = [forced]
+            else:
+                modes = ["nocarry", "carry" if B >= 256 else "early"]
+            for m in modes:
+                cands.append(("rccl" if m == "carry" else f"rccl-{m}", red, m, True))
+        elif name == "xgmi" and model == "cnn":
+            cands.append(("xgmi", red, "carry", True))
+            if exchange_step and red.exchange_ok(1):
+                cands.append(("xgmi-noxchg", red, "carry", False))
         else:
-            cands.append((name, red, "carry"))
+            cands.append((name, red, "carry", True))
     return cands
 
 
@@ -164,7 +187,7 @@ class _DryStep(Candidate):
     (PDM_CALIB_FAULT="<rank>:<name>:<phase>": setup / warm / timed / check raise, diverge
     perturbs this rank's replica, hang stalls the device sync until its deadline)."""
 
-    COST_MS = {"xgmi": 1.0, "rccl": 0.6, "rccl-nocarry": 0.8, "rccl-side": 0.7,
+    COST_MS = {"xgmi": 1.0, "xgmi-noxchg": 0.7, "rccl-nocarry": 0.8, "rccl": 0.6,
                "rccl-early": 0.4}
 
     def __init__(self, name, rank, state, faults):
@@ -288,18 +311,31 @@ def main():
     want = knobs.get("PDM_COMM", "auto")
     reducers = {}
     notes = []
-    if (ws > 1 or force_comm) and want == "auto" and isinstance(comm, parallel.RcclComm):
+    # every xgmi device wait for a peer gives up after xg_timeout (error word, fail-fast); a
+    # calibration candidate's host deadline is strictly longer, so a transport that hangs on
+    # the device ends there, is read from its error word and dropped -- the RCCL communicator
+    # is only aborted for a hang no device deadline bounds (an RCCL candidate)
+    xg_timeout = float(knobs.get("PDM_XGMI_TIMEOUT", "30"))
+    calib_timeout = xg_timeout + float(knobs.get("PDM_CALIB_TIMEOUT_S", "30"))
+    # the one-GPU rehearsal (gloo data plane, ranks sharing device 0) calibrates the direct
+    # xGMI transport against the gloo reducer, as the real node does against RCCL
+    rehearsal = ws > 1 and knobs.get("PDM_SHARE_DEVICE") == "1" and \
+        isinstance(comm, parallel.TorchComm) and model == "cnn"
+    if (ws > 1 or force_comm) and want == "auto" and \
+            (isinstance(comm, parallel.RcclComm) or rehearsal):
         try:
             reducers["xgmi"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
-                                                    transport="xgmi", channels=channels)
+                                                    transport="xgmi", channels=channels,
+                                                    timeout_s=xg_timeout)
         except Exception as e:                # collective decision: no rank uses xgmi
             notes.append(f"xgmi unavailable: {e}")
             print(f"bench.py: xgmi transport unavailable: {e}", file=sys.stderr, flush=True)
-        reducers["rccl"] = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
-                                                transport="rccl")
+        r1 = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm,
+                                  transport="rccl")
+        reducers[r1.kind] = r1
     else:
         r0 = parallel.GradReducer(comm, arena.grads, bounds, force=force_comm, transport=want,
-                                  channels=channels)
+                                  channels=channels, timeout_s=xg_timeout)
         reducers[r0.kind] = r0
         if r0.transport_note:
             notes.append(r0.transport_note)
@@ -311,10 +347,6 @@ def main():
 
     def sync(what):
         parallel.bounded_sync(device, a.timeout, comm, what)
-
-    # a calibration candidate that hangs on the device is cut off sooner than the run's own
-    # deadline (the communicator is then aborted and the run ends with the reason)
-    calib_timeout = min(a.timeout, float(knobs.get("PDM_CALIB_TIMEOUT_S", "60")))
 
     def barrier():
         parallel.control_barrier()      # gloo (CPU tensor): no torch NCCL communicator
@@ -406,7 +438,7 @@ def main():
 
         shardable = hasattr(prog.gpu, "set_shard_fc")
 
-        def use(red, carry="carry"):
+        def use(red, carry="carry", xchg=True):
             if shardable:
                 prog.gpu.set_shard_fc(False)   # (gathers the sharded state on the old reducer)
             prog.reducer = red
@@ -414,6 +446,8 @@ def main():
             prog.gpu.use_graphs = bool(a.graphs) and red.capturable
             if hasattr(prog.gpu, "set_rccl_mode"):
                 prog.gpu.set_rccl_mode(carry, invalidate=False)
+            if hasattr(prog.gpu, "xgmi_exchange"):
+                prog.gpu.xgmi_exchange = bool(xchg) and prog.structure.xgmi_exchange
             prog.gpu.invalidate_graphs()
             if shardable and (carry == "zero" or knobs.get("PDM_SHARD_FC") == "1") and \
                     red.active and prog.gpu.shard_supported():
@@ -426,8 +460,10 @@ def main():
             if tail:
                 prog.gpu.prepare(tail, sizes=(1,))
 
-        cands = step_candidates(reducers, model,
-                                lambda red: shardable and prog.gpu.shard_supported(red))
+        cands = step_candidates(reducers, model, B,
+                                lambda red: shardable and prog.gpu.shard_supported(red),
+                                exchange_step=hasattr(prog.gpu, "xgmi_exchange") and
+                                prog.structure.xgmi_exchange)
 
         def fingerprint():
             """Bits of this rank's replica (master weights + optimizer state)."""
@@ -437,7 +473,19 @@ def main():
 
         def recover():
             """After a failed candidate: drain, leave sharding, and restore every replica
-            (weights, momentum, bf16 compute copies) from rank 0."""
+            (weights, momentum, bf16 compute copies) from rank 0.  A host deadline that had
+            to abort the RCCL communicator (a hang no device deadline bounds) on any rank
+            leaves every rank's communicator unusable: every rank then drains its device
+            and joins a fresh communicator (RcclComm.revive), and the RCCL reducer is rebuilt
+            on it, so the remaining candidates and the timed run keep their data plane."""
+            alive = not isinstance(comm, parallel.RcclComm) or comm.alive
+            if not ControlPlane(ws).agree(alive):
+                parallel.bounded_sync(device, a.timeout, None, "recovery (drain after abort)")
+                comm.revive()
+                for r in reducers.values():
+                    r.rebind()
+                print(f"bench.py: rank {rank}: RCCL communicator re-created after an abort",
+                      file=sys.stderr, flush=True)
             sync("recovery")
             if shardable:
                 prog.gpu.set_shard_fc(False)
@@ -447,19 +495,39 @@ def main():
                 prog.gpu.refresh_shadows()     # bf16 compute copies of the weights
             sync("recovery broadcast")
 
+        faults = knobs.get("PDM_CALIB_FAULT") or ""
+
+        def device_fault(name, kind):
+            """PDM_CALIB_FAULT "<rank>:<candidate>:devhang|spin" on this rank (a real device
+            hang: the xgmi collective never launched; or a bounded device stall past the host
+            deadline)."""
+            return f"{rank}:{name}:{kind}" in faults.split(",")
+
         class Step(Candidate):
-            def __init__(self, name, red, carry):
-                self.name, self.red, self.carry = name, red, carry
+            def __init__(self, name, red, carry, xchg):
+                self.name, self.red, self.carry, self.xchg = name, red, carry, xchg
 
             def setup(self):
-                use(self.red, self.carry)
+                self.red.fault_no_collective = device_fault(self.name, "devhang")
+                use(self.red, self.carry, self.xchg)
+                # xgmi: the candidates before this one left the transport's counters where
+                # their structure (or a device deadline) left them; every rank re-arms it
+                # here, and the setup agreement orders that before any rank's first launch
+                self.red.reset_transport()
                 prepare()                      # capture outside the calibration window
 
             def enqueue(self, k):
-                return run(k)
+                n = run(k)
+                if device_fault(self.name, "spin"):
+                    prog.gpu.C.debug_spin(min(30.0, calib_timeout + 2.0))
+                return n
 
             def sync(self):
-                parallel.bounded_sync(device, calib_timeout, comm, f"calibration ({self.name})")
+                # the xgmi transport's device waits are bounded by xg_timeout < calib_timeout:
+                # its hang drains by itself (error word, read in check()), so the deadline
+                # leaves the communicator alone; an RCCL hang needs the abort to drain
+                parallel.bounded_sync(device, calib_timeout, comm, f"calibration ({self.name})",
+                                      abort=self.red.kind != "xgmi")
 
             def check(self):
                 self.red.check()
@@ -472,7 +540,7 @@ def main():
 
         opt.sync_hyperparams()
         next_epoch()
-        steps = {name: Step(name, red, carry) for name, red, carry in cands}
+        steps = {name: Step(name, red, carry, xchg) for name, red, carry, xchg in cands}
         calib = {}
         if len(cands) > 1:
             cal = calibrate(list(steps.values()), ControlPlane(ws), rank,
@@ -484,7 +552,11 @@ def main():
             best = cal.best
         else:
             best = cands[0][0]
-        use(steps[best].red, steps[best].carry)
+        for st in steps.values():
+            st.red.fault_no_collective = False
+        use(steps[best].red, steps[best].carry, steps[best].xchg)
+        steps[best].red.reset_transport()
+        parallel.control_barrier()           # every rank re-armed before any launches
         chosen = prog.reducer
         prepare()
         # put the next epoch boundary inside the timed window: continue the current epoch

@@ -411,6 +411,12 @@ void xgmi_wait(at::Tensor sync, int64_t signal_ch, std::vector<int64_t> waits, d
                    cur_stream(sync));
 }
 
+// fault injection (bench.py calibration tests): a bounded device stall on the current stream
+void debug_spin(double seconds) {
+  TORCH_CHECK(seconds > 0 && seconds <= 30, "debug_spin: 0 < seconds <= 30");
+  launch_debug_spin((long long)(seconds * 1e8), c10::hip::getCurrentHIPStream().stream());
+}
+
 // ------------------------------------------------------------------ CNN (bf16)
 void need_min(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* name) {
   need(t, dt, name);
@@ -573,44 +579,6 @@ void cnn_head(at::Tensor part, int64_t splitk, int64_t B, at::Tensor bf1, at::Te
                   train ? xg_step(xg) : nullptr, pdh32, cur_stream(part));
 }
 
-// fc1_fwd + training head in one launch (kernels.h launch_fc1_head); same arguments as the
-// two, plus `sync` (int32 [4], zeroed once; the kernel re-arms it) and the wait bound
-void fc1_head(at::Tensor pool, at::Tensor wf1, at::Tensor part, int64_t B, int64_t splitk,
-              at::Tensor bf1, at::Tensor wf2, at::Tensor bf2, at::Tensor ylab, at::Tensor dh,
-              at::Tensor dht, int64_t ldt, at::Tensor slab, at::Tensor metrics,
-              c10::optional<at::Tensor> c0, c10::optional<at::Tensor> c1, at::Tensor sync,
-              c10::optional<at::Tensor> xg, double timeout_s) {
-  c10::DeviceGuard g(pool.device());
-  TORCH_CHECK(B >= 1, "B must be >= 1");
-  TORCH_CHECK(ldt % 32 == 0 && ldt >= B, "ldt must be a multiple of 32 and >= B");
-  TORCH_CHECK(fc1_head_grid((int)B, (int)splitk, (int)ldt) > 0,
-              "fc1_head: (B, splitk, ldt) = (", B, ", ", splitk, ", ", ldt,
-              ") needs separate fc1_fwd / cnn_head launches (fc1_head_grid == 0)");
-  need_min(pool, at::kBFloat16, B * CNN_FEAT, "pool");
-  need_min(wf1, at::kBFloat16, (int64_t)CNN_HID * CNN_FEAT, "wf1");
-  need_min(part, at::kFloat, splitk * B * CNN_HID, "part");
-  need_min(bf1, at::kFloat, CNN_HID, "bf1");
-  need_min(wf2, at::kFloat, CNN_NCLS * CNN_HID, "wf2");
-  need(bf2, at::kFloat, "bf2");
-  TORCH_CHECK(bf2.numel() == CNN_NCLS, "bf2");
-  need(ylab, at::kInt, "ylab");
-  need_min(ylab, at::kInt, B, "ylab");
-  need_min(dh, at::kBFloat16, ldt * CNN_HID, "dh");
-  need_min(dht, at::kBFloat16, ldt * CNN_HID, "dht");
-  need_min(slab, at::kFloat, (int64_t)cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)) * CNN_HEAD_SLAB,
-           "head slab");
-  need(metrics, at::kDouble, "metrics");
-  need_numel(metrics, 3, "metrics");
-  need(sync, at::kInt, "sync");
-  need_numel(sync, 4, "sync");
-  TORCH_CHECK(timeout_s > 0, "timeout_s must be > 0");
-  launch_fc1_head(ptr<__bf16>(pool), ptr<__bf16>(wf1), part.data_ptr<float>(), (int)B, (int)splitk,
-                  bf1.data_ptr<float>(), wf2.data_ptr<float>(), bf2.data_ptr<float>(),
-                  ylab.data_ptr<int32_t>(), ptr<__bf16>(dh), ptr<__bf16>(dht), (int)ldt,
-                  slab.data_ptr<float>(), metrics.data_ptr<double>(), opt_i64(c0), opt_i64(c1),
-                  xg_step(xg), reinterpret_cast<unsigned*>(sync.data_ptr()),
-                  (long long)(timeout_s * 1e8), cur_stream(pool));
-}
 
 // fc_update (world size 1, optional): (kind, p, g, m, v or None, shadow, lr, step, beta1,
 // beta2, eps, wd, momentum, dampening, nesterov, grad_scale[, shadow_t_next]) -- the
@@ -925,6 +893,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out_images"), py::arg("out_labels"), py::arg("ctr") = py::none(),
         py::arg("step") = py::none(), py::arg("step_value") = 0, py::arg("max_wgs") = 0);
   m.def("xgmi_wait", &xgmi_wait);
+  m.def("debug_spin", &debug_spin, py::arg("seconds"));
   m.attr("CNN_HEAD_ROWS") = CNN_HEAD_ROWS;
   m.def("cnn_head_nblk", [](int64_t ldt) { return cnn_head_blocks((int)(ldt / CNN_HEAD_ROWS)); });
   m.attr("CNN_HEAD_SLAB") = CNN_HEAD_SLAB;
@@ -939,14 +908,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fc_carry") = py::none(), py::arg("fc_carry_wait") = py::none());
   m.def("fc1_fwd", &fc1_fwd);
   m.attr("FC1_BIG_B") = FC1_BIG_B;
-  m.def("fc1_head", &fc1_head, py::arg("pool"), py::arg("wf1"), py::arg("part"), py::arg("B"),
-        py::arg("splitk"), py::arg("bf1"), py::arg("wf2"), py::arg("bf2"), py::arg("ylab"),
-        py::arg("dh"), py::arg("dht"), py::arg("ldt"), py::arg("slab"), py::arg("metrics"),
-        py::arg("c0"), py::arg("c1"), py::arg("sync"), py::arg("xg") = py::none(),
-        py::arg("timeout_s") = 2.0);
-  m.def("fc1_head_grid", [](int64_t B, int64_t splitk, int64_t ldt) {
-    return fc1_head_grid((int)B, (int)splitk, (int)ldt);
-  });
   m.def("cnn_head", &cnn_head, py::arg("part"), py::arg("splitk"), py::arg("B"), py::arg("bf1"),
         py::arg("wf2"), py::arg("bf2"), py::arg("ylab"), py::arg("train"), py::arg("dh"),
         py::arg("dht"), py::arg("ldt"), py::arg("slab"), py::arg("metrics"), py::arg("c0"),

@@ -83,17 +83,18 @@ __device__ __forceinline__ float from_bf16(bf16 h) { return (float)h; }
 // boundary (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s).  Agent-scope
 // write-through stores (global_store ... sc1) send them to memory as they are stored,
 // beside the kernel's other work; the readers are other workgroups on other XCDs, so no
-// L2 locality is given up.  PDM_WT selects the site groups (a bitmask, build time):
-//   1 conv gradient slabs (cnn_bwd[_band] -> optimizer / conv_reduce)
+// L2 locality is given up.  The site groups (G):
+//   1 conv gradient slabs (cnn_bwd[_band] -> optimizer / conv_reduce): write-through
 //   2 fc1_bwd outputs (dpool, the fc1 gradient, the fused update's weights and copies)
 //   4 cnn_fwd[_band] outputs (pool, mask, image, a1 / x hand-offs)
 //   8 fc1_fwd split-K partials and cnn_head outputs (dh, dh^T, head slabs)
-#ifndef PDM_WT
-#define PDM_WT 1
-#endif
+// Only group 1 is stored write-through: the others were measured neutral or slower that way
+// (round 5, profiles/r5/wt/): the next launch reads them on the writer's XCD often enough
+// that the L2 copy helps.  (The build-time group mask that measured it was removed in round 6.)
+constexpr int PDM_WT_GROUPS = 1;
 template <int G, class T>
 __device__ __forceinline__ void st_ho(T* p, T v) {
-  if constexpr ((PDM_WT & G) == 0) {
+  if constexpr ((PDM_WT_GROUPS & G) == 0) {
     *p = v;
   } else if constexpr (sizeof(T) == 16) {
     unsigned long long w[2];
@@ -114,22 +115,10 @@ __device__ __forceinline__ void st_ho(T* p, T v) {
   }
 }
 
-// Stores of per-workgroup gradient slabs (read once, by the next launch).  PDM_NT=1
-// (diagnostic builds): streaming (non-temporal) stores and loads for them.
-#ifndef PDM_NT
-#define PDM_NT 0
-#endif
-__device__ __forceinline__ void pdm_slab_store(float* p, float v) {
-  if (PDM_NT == 1) __builtin_nontemporal_store(v, p);
-  else st_ho<1>(p, v);
-}
-__device__ __forceinline__ float4 pdm_slab_load4(const float4* p) {
-  if (PDM_NT == 1) {
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    return make_float4(v[0], v[1], v[2], v[3]);
-  }
-  return *p;
-}
+// Stores / loads of per-workgroup gradient slabs (read once, by the next launch).
+// Non-temporal (streaming) forms of both measured slower (round 4, docs/kernels.md).
+__device__ __forceinline__ void pdm_slab_store(float* p, float v) { st_ho<1>(p, v); }
+__device__ __forceinline__ float4 pdm_slab_load4(const float4* p) { return *p; }
 
 // Bookkeeping done by exactly one thread of a kernel that no other kernel of the
 // same step reads concurrently (see runtime/gpu_step.py: the "middle" kernel

@@ -28,10 +28,8 @@ __host__ __device__ __forceinline__ int64_t step_row(const StepRows g, int64_t n
 // ---------------------------------------------------------------- linear model
 constexpr int LIN_K = 784;
 constexpr int LIN_N = 10;
-#ifndef PDM_LIN_ROWS
-#define PDM_LIN_ROWS 4   // train rows per workgroup (us/step at B = 256, Adam: 1: 17.8, 2: 13.8, 4: 12.4, 8: 13.7, 16: 17.1)
-#endif
-constexpr int LIN_ROWS = PDM_LIN_ROWS;
+// train rows per workgroup (us/step at B = 256, Adam: 1: 17.8, 2: 13.8, 4: 12.4, 8: 13.7, 16: 17.1)
+constexpr int LIN_ROWS = 4;
 constexpr int LIN_SLAB = 7856;  // 7840 dW + 10 db + loss + correct, padded
 constexpr int LIN_EVAL_ROWS = 16;
 
@@ -218,17 +216,6 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
                      const float* bf2, const int32_t* ylab, bool train, __bf16* dh, __bf16* dht,
                      int ldt, float* slab, double* metrics, int64_t* c0, int64_t* c1,
                      unsigned* c2, float* dh32, hipStream_t st);
-// fc1_fwd + the training head in one launch (cnn_fwd.hip fc1_head_kernel): its grid, or 0 when
-// (B, splitk, ldt) needs the two launches (128-row blocks, or more workgroups than the chip
-// holds at once: a head workgroup waits for every split-K workgroup).  sync: 4 zeroed words
-// (arrival count, head passes, error bit, spare) owned by the caller; timeout in
-// s_memrealtime ticks (100 MHz)
-constexpr int FC1_HEAD_MAX_GRID = 384;
-int fc1_head_grid(int B, int splitk, int ldt);
-void launch_fc1_head(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
-                     const float* bf1, const float* wf2, const float* bf2, const int32_t* ylab,
-                     __bf16* dh, __bf16* dht, int ldt, float* slab, double* metrics, int64_t* c0,
-                     int64_t* c1, unsigned* c2, unsigned* sync, long long timeout, hipStream_t st);
 void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* pool,
                     const __bf16* wf1t, int B, float* gwf1, __bf16* dpool, const float* head_slab,
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,

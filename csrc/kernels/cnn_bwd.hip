@@ -69,10 +69,7 @@ constexpr int DW_MT = PDM_DW_MT;
 static_assert(DW_MT == 1 || DW_MT == 2, "dW tile: 64 or 128 hidden rows");
 constexpr int DW_FT = FEAT / 64;                      // 144 feature tiles
 constexpr int DW_TILES = DW_FT * (2 / DW_MT);         // 144 or 288
-#ifndef PDM_DWC
-#define PDM_DWC 128
-#endif
-constexpr int DWC = PDM_DWC;         // dW1 batch rows staged per LDS round
+constexpr int DWC = 128;             // dW1 batch rows staged per LDS round
 constexpr int DX_COLS = 384;         // dX tile: 32 batch rows x 384 features per workgroup
 constexpr int DX_TILES = FEAT / DX_COLS;   // 24 = 8 XCDs x 3
 constexpr int DX_FT = DX_COLS / 64;        // 16-feature sub-tiles per wave (6)
@@ -91,11 +88,8 @@ __device__ __forceinline__ int tile_off(int row, int byte) {
 // Two waves per SIMD, i.e. two workgroups per CU (<= 256 registers per lane; 162 VGPRs, no
 // spill): the 503 workgroups at B = 256 (288 dW + 192 dX + 23 head-slab) run in one round
 // instead of two.  fc1_bwd 10.0 -> 9.6 us, the B = 256 step 54.9 -> 53.9 us (interleaved A/B,
-// profiles/r5/fc1bwd_wpe2).  PDM_FC1BWD_WPE=1: the old bound (260 registers, one per CU).
-#ifndef PDM_FC1BWD_WPE
-#define PDM_FC1BWD_WPE 2
-#endif
-__global__ __launch_bounds__(256, PDM_FC1BWD_WPE) void fc1_bwd_kernel(
+// profiles/r5/fc1bwd_wpe2).
+__global__ __launch_bounds__(256, 2) void fc1_bwd_kernel(
     const bf16* __restrict__ dh, const bf16* __restrict__ dht, int ldt,
     const bf16* __restrict__ pool, const bf16* __restrict__ wf1t, int B, float* __restrict__ gwf1,
     bf16* __restrict__ dpool, const float* __restrict__ head_slab, int head_blocks,
@@ -523,7 +517,9 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   int tb[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) tb[j] = toff[j] == IMG * IMG ? 0 : toff[j];   // w = 0 there
-  const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);   // mt = 0; mt = 1: ^ 32
+  // one 16-B store per lane and tile: lane pairs g, g ^ 1 swap channel halves
+  // (cnn_common.h conv1_pair)
+  const int a1c = (conv1_pair_chunk(g) ^ (i16 & 3)) << 4;
   bf16x4 bx[TPW];
   int vv[TPW];
 #pragma unroll
@@ -537,16 +533,16 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   for (int k = 0; k < TPW; ++k) {
     const int y = vv[k] / IMG, x = vv[k] - y * IMG;
     const bool ok = y < H1 && x < H1;
-    const int ab = (vv[k] - 2 * y) * 64 + a1c;
+    bf16x4 o[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-      bf16x4 o = {to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
-                  to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
-      // dropped pixels store into the spare LDS tail: no branch
-      const int dst = ok ? B_A1 + (ab ^ (32 * mt)) : B_SPARE + lane * 8;
-      *reinterpret_cast<bf16x4*>(smem + dst) = o;
+      o[mt] = bf16x4{to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
+                     to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
     }
+    // dropped pixels store into the spare LDS tail (lane pairs share a 16-B slot): no branch
+    const int dst = ok ? B_A1 + (vv[k] - 2 * y) * 64 + a1c : B_SPARE + (lane & 31) * 16;
+    *reinterpret_cast<uint4*>(smem + dst) = conv1_pair(o[0], o[1]);
   }
   if (threadIdx.x == 0) PDM_STAMP_VAL(14, PDM_CLOCK());
   // ---- 4. the dz2 scatter
@@ -683,12 +679,8 @@ __device__ __forceinline__ void dgrad_pass(const char* smem, int tile0, const in
 #pragma unroll
   for (int tk = 0; tk < 18; ++tk) {
     __builtin_amdgcn_sched_barrier(0);   // keep each step's reads where they are issued
-#if PDM_ABL == 3
-    if (tk + PFD == 18) read_ep();   // timing ablation: no operand reads in the step loop
-#else
     if (tk + PFD < 18) read_step(tk + PFD, a[(tk + PFD) % (PFD + 1)], w[(tk + PFD) % (PFD + 1)]);
     else if (tk + PFD == 18) read_ep();
-#endif
     // the reads go out before this step's MFMAs (hipcc otherwise sinks them below the
     // MFMAs and the read-ahead shrinks to ~1 step: lgkmcnt(7) instead of lgkmcnt(12))
     __builtin_amdgcn_sched_barrier(0);
@@ -726,17 +718,8 @@ __device__ __forceinline__ void dgrad_pass(const char* smem, int tile0, const in
 // ci-tile) pairs), waves 4-7 the dgrad over 48 tile slots (46 of the 28-wide virtual grid)
 // in passes of DG_MTP tiles with operands read DG_PFD steps ahead; with one image per
 // workgroup the wgrad waves run the third dgrad pass after their wgrad.
-#ifndef PDM_ABL
-#define PDM_ABL 0     // diagnostic builds only: 1 skip wgrad, 2 skip dgrad, 3 dgrad without reads
-#endif
-#ifndef PDM_DG_MTP
-#define PDM_DG_MTP 4
-#endif
-#ifndef PDM_DG_PFD
-#define PDM_DG_PFD 2
-#endif
-constexpr int DG_MTP = PDM_DG_MTP;       // tiles per dgrad pass on waves 4-7
-constexpr int DG_PFD = PDM_DG_PFD;       // read-ahead distance in (tap, K-half) steps
+constexpr int DG_MTP = 4;       // tiles per dgrad pass on waves 4-7
+constexpr int DG_PFD = 2;       // read-ahead distance in (tap, K-half) steps
 static_assert(12 % DG_MTP == 0, "dgrad passes: 12 / DG_MTP passes of DG_MTP tiles per wave (the "
               "wgrad waves take the last pass when a workgroup has one image)");
 static_assert(DG_PFD * (DG_MTP + 2) <= 15, "in-flight LDS reads must fit lgkmcnt");
@@ -866,7 +849,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
       PDM_STAMP(1);
-      if (img < B && PDM_ABL != 1) wgrad_image();   // PDM_ABL: timing ablations only
+      if (img < B) wgrad_image();
       PDM_STAMP(2);
       if (last) {
 #pragma unroll
@@ -888,7 +871,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
       // last dgrad pass (tiles 48 - 4 DG_MTP + wave + 4k), which balances the two wave groups (the
       // wgrad's 360 MFMAs vs the dgrad's 432 + epilogues)
       if constexpr (decltype(one)::value) {
-        if (img < B && PDM_ABL != 2)
+        if (img < B)
           dgrad_pass<DG_MTP, DG_PFD>(smem, 48 - 4 * DG_MTP + wave, ka1, acc1, t_mf, t_ep);
       }
       __syncthreads();
@@ -909,7 +892,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
       const int img = blockIdx.x * ipb + i;
       if (img < B) bwd_load_image<decltype(first)::value>(smem, img, xg, dpool, pmask, w1, b1, w2t, db2p);
       __syncthreads();
-      if (img < B && PDM_ABL != 2) {
+      if (img < B) {
         // tiles wd + 4j, j < 12, in passes of DG_MTP tiles; a rolled pass loop keeps one
         // copy of the pass code and stops cross-pass scheduling
         // (one image per workgroup: the wgrad waves take the last pass)
@@ -1024,16 +1007,7 @@ void launch_fc1_bwd(const __bf16* dh, const __bf16* dht, int ldt, const __bf16* 
                     int head_blocks, float* gwf2, float* gbf2, float* gbf1, double* metrics,
                     const FcUpdate& fcu, hipStream_t st) {
   const int nd = (ldt / 32) * DX_TILES;
-  int nblk = DW_TILES + nd + HR_BLOCKS, off = 0;
-#ifdef PDM_DIAG_ROLES
-  // diagnostic builds only (tools/kbench_fc.py): PDM_FC1BWD_ROLE=dw|dx|hr launches one
-  // role alone.  Never compiled into the production extension: a stray environment
-  // variable there would silently skip gradient work (and the fused fc1 update).
-  static const char* role = getenv("PDM_FC1BWD_ROLE");
-  if (role && role[0] == 'd' && role[1] == 'w') nblk = DW_TILES;
-  else if (role && role[0] == 'd' && role[1] == 'x') { nblk = nd; off = DW_TILES; }
-  else if (role && role[0] == 'h') { nblk = HR_BLOCKS; off = DW_TILES + nd; }
-#endif
+  const int nblk = DW_TILES + nd + HR_BLOCKS, off = 0;
   fc1_bwd_kernel<<<nblk, 256, 0, st>>>(dh, dht, ldt, pool, wf1t, B, gwf1, dpool, head_slab,
                                        head_blocks, gwf2, gbf2, gbf1, metrics, off, fcu);
 }

@@ -62,6 +62,23 @@ __device__ __forceinline__ int a1_off(int row, int col, int byte) {
   return (row * H1 + col) * 64 + ((((byte >> 4) ^ (col & 3))) << 4) + (byte & 15);
 }
 
+// conv1 epilogue (D[co][pixel] on mfma_f32_16x16x16_bf16): lane (g = lane >> 4, i16) holds
+// channels 4g .. 4g + 3 of pixel i16 for both 16-channel halves (o0: co < 16, o1: co >= 16).
+// Two 8-B stores per lane at a 64-B pixel stride were 4-way bank conflicts (ds_write_b64:
+// 16 contiguous lanes per LDS cycle, one chunk slot per pixel residue mod 4).  Lane pairs
+// g, g ^ 1 swap halves on gfx950's v_permlane16_swap (odd rows of the first operand <-> even
+// rows of the second), so every lane holds 8 consecutive channels and issues ONE 16-B store:
+// even g: channels 4g .. 4g + 7, odd g: 16 + 4(g - 1) .. + 7 -- the 16-B chunk
+// conv1_pair_chunk(g) of the pixel (ds_write_b128: 8 contiguous lanes per cycle, 2-way).
+// Full EXEC required.
+__device__ __forceinline__ uint4 conv1_pair(bf16x4 o0, bf16x4 o1) {
+  const uint2 u0 = __builtin_bit_cast(uint2, o0), u1 = __builtin_bit_cast(uint2, o1);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(u0.x, u1.x, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(u0.y, u1.y, false, false);
+  return make_uint4(r0[0], r1[0], r0[1], r1[1]);
+}
+__device__ __forceinline__ int conv1_pair_chunk(int g) { return (g >> 1) | ((g & 1) << 1); }
+
 // LDS image of dz2 = dL/d(conv2 pre-activation) (24x24 x 64 bf16 = 128 B/pixel).
 // Chunk swizzle (2*row + col) & 7: conflict-free ds_read_b128 for the dgrad A rows,
 // 2-way for the wgrad ds_read_b64_tr_b16 column reads (searched, see docs/kernels.md).

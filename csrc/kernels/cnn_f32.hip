@@ -338,11 +338,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[nt][r] = ws[288 + 16 * nt + 4 * g + r];
     const int a1c = (((g >> 1) ^ (i16 & 3)) << 4) + 8 * (g & 1);   // nt = 0; nt = 1: ^ 32
-#if defined(PDM_ABL) && PDM_ABL == 22     // timing ablation only: no conv1
-    for (int tile = wave; tile < 0; tile += 8) {
-#else
     for (int tile = wave; tile < (IMG * H1 + 15) / 16; tile += 8) {
-#endif
       const int V = tile * 16 + i16;
       float xb[3];
 #pragma unroll
@@ -367,13 +363,11 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
           const int off = ab ^ (32 * nt);
           *reinterpret_cast<bf16x4*>(smem + XF_AH + off) = h;
           *reinterpret_cast<bf16x4*>(smem + XF_AL + off) = l;
-#if !defined(PDM_ABL) || PDM_ABL != 21     // timing ablation only: no a1 hand-off writes
           if (TRAIN) {
             char* dst = a1x + (int64_t)img * 2 * A1X_PLANE + off;
             *reinterpret_cast<bf16x4*>(dst) = h;
             *reinterpret_cast<bf16x4*>(dst + A1X_PLANE) = l;
           }
-#endif
         }
       }
     }
@@ -407,11 +401,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_fwd_kernel(
   };
   bf16x8 ch = *reinterpret_cast<const bf16x8*>(smem + XF_AH + tile_base(tt0) + aoff[0]);
   bf16x8 cl = *reinterpret_cast<const bf16x8*>(smem + XF_AL + tile_base(tt0) + aoff[0]);
-#if defined(PDM_ABL) && PDM_ABL == 23     // timing ablation only: no conv2
-  for (int tt = tt0; tt < tt0; ++tt) {
-#else
   for (int tt = tt0; tt < tt1; ++tt) {
-#endif
     const int py = tt / 3, px0 = 4 * (tt - py * 3);
     const int tb = tile_base(tt), nb = tile_base(min(tt + 1, tt1 - 1));
     f32x4 acc[2];
@@ -1324,11 +1314,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     // 4 pixels in both planes (the pooled gradient at the channel's argmax if it was
     // positive, zero elsewhere): 8 ds_write_b128 per item instead of zeroing 60 KB and
     // 2-byte stores.  Mask byte (f32x3_fwd): 0x80 | 1 << s if the pooled value is > 0, else 0
-#if !defined(PDM_ABL) || PDM_ABL != 13   // timing ablation only (wrong results)
     if (tid < nsc / 8) {
-#else
-    if (tid < 0) {
-#endif
       const int pl = tid >> 3, c = tid & 7;
       const int py = pr0 + pl / HP, px = pl - (pl / HP) * HP;
       const float v[8] = {dq0.x, dq0.y, dq0.z, dq0.w, dq1.x, dq1.y, dq1.z, dq1.w};
@@ -1371,11 +1357,7 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     __syncthreads();
     if (first) PDM_STAMP(11);
     // ---- conv2 dgrad over the band's own a1 pixels + relu'(a1) + conv1 weight/bias grad
-#if defined(PDM_ABL) && PDM_ABL == 11
-    for (int mt = wave; mt < 0; mt += 8) {
-#else
     for (int mt = wave; mt < nmt; mt += 8) {
-#endif
       const int p = min(mt * 16 + i16, npx - 1);
       const int y = p / H1, x = p - y * H1;
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -1439,9 +1421,6 @@ __global__ __launch_bounds__(FT, 1) void f32x3_conv_bwd_kernel(
     // ---- conv2 wgrad over the band's 96 own output pixels (3 k-steps of 32): k-run
     // v = 4 ks + g (8 pixels of output row v / 3, columns 8 (v % 3) ..); lane (g, q, pq) gives
     // the addresses of pixels col0 + q and col0 + 4 + q of that run, columns 4 pq .. 4 pq + 3
-#if defined(PDM_ABL) && PDM_ABL == 12
-    if (npx < 0)
-#endif
     {
       // 27 steps (k-step ks, column j), software-pipelined like the dgrad: the B pieces of
       // step s + 1 and (two steps before a k-step starts) its A pieces are read, pinned by a

@@ -29,11 +29,9 @@
 #if defined(PDM_STAMPS)
 #define PDM_WANT_FC1_FWD (PDM_FWD_TU == 0)
 #define PDM_WANT_HEAD (PDM_FWD_TU == 0)
-#define PDM_WANT_FC1_HEAD (PDM_FWD_TU == 0)
 #else
 #define PDM_WANT_FC1_FWD (PDM_FWD_TU == 1)
 #define PDM_WANT_HEAD (PDM_FWD_TU == 2)
-#define PDM_WANT_FC1_HEAD (PDM_FWD_TU == 3)
 #endif
 #define PDM_WANT_FWD_REST (PDM_FWD_TU == 0)
 
@@ -172,12 +170,8 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   auto load_wb = [&](int f) {   // fragments 3f .. 3f+2 of the 18 (tap, n-tile) pairs
 #pragma unroll
     for (int e = 3 * f; e < 3 * f + 3; ++e)
-#if defined(PDM_ABL) && PDM_ABL == 4   // timing ablation only: no conv2 weight loads
-      wb[e >> 1][e & 1] = bf16x8{};
-#else
       wb[e >> 1][e & 1] = *reinterpret_cast<const bf16x8*>(   // fragment-major W2 (frag_pos)
           w2 + ((int64_t)((nh * 2 + (e & 1)) * 9 + (e >> 1)) * 64 + lane) * 8);
-#endif
   };
 
   bf16x4 w1f[2];
@@ -193,7 +187,9 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
   {
     constexpr int TPW = 6;
     const int rowg = IMG * (g < 3 ? g : 0);   // lane group 3: zero weights, any finite x
-    const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);   // mt = 0; mt = 1: ^ 32
+    // one 16-B store per lane and tile: lane pairs g, g ^ 1 swap channel halves
+    // (cnn_common.h conv1_pair)
+    const int a1c = (conv1_pair_chunk(g) ^ (i16 & 3)) << 4;
     // two rounds of 3 tiles: the 72 conv2 B-fragment registers are live here, and 6 tiles'
     // operands at once would push the kernel past 128 VGPRs (2 workgroups / CU)
 #pragma unroll
@@ -210,16 +206,16 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
       load_wb(k);
       const int y = vv[k] / IMG, x = vv[k] - y * IMG;
       const bool ok = y < H1 && x < H1;
-      const int ab = (vv[k] - 2 * y) * 64 + a1c;
+      bf16x4 o[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-        bf16x4 o = {to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
-                    to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
-        // dropped pixels store into the (not yet used) pooled-output area: no branch
-        const int dst = ok ? F_A1 + (ab ^ (32 * mt)) : F_PS + lane * 8;
-        *reinterpret_cast<bf16x4*>(smem + dst) = o;
+        o[mt] = bf16x4{to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
+                       to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
       }
+      // dropped pixels store into the (not yet used) pooled-output area: no branch
+      const int dst = ok ? F_A1 + (vv[k] - 2 * y) * 64 + a1c : F_PS + lane * 16;
+      *reinterpret_cast<uint4*>(smem + dst) = conv1_pair(o[0], o[1]);
     }
     }
   }
@@ -293,7 +289,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 }
 
 #endif  // PDM_WANT_FWD_REST
-#if PDM_WANT_FC1_FWD || PDM_WANT_FC1_HEAD
+#if PDM_WANT_FC1_FWD
 // ---- fc1 forward: split-K GEMM, 32 MT rows x 128 cols per block ----
 // KB = k-steps per load batch: 9 (288 k-steps = 32 batches; split factors dividing 32) or 3
 // (96 batches: split factors up to 96, so B <= 64 can put W1 on ~256 CUs instead of 32-64)
@@ -301,8 +297,7 @@ __global__ __launch_bounds__(FWD_THREADS, 2) void cnn_fwd_kernel(
 // tiles every block streams its whole K slice of W1 from L2 for 32 rows only (B = 8192,
 // split-K 1: 256 x 2.4 MB = 604 MB of L2 reads, 80 us); 128-row tiles read W1 a quarter as
 // often and leave the pool read from HBM as the bound
-// WT: the partials are stored write-through (sc1), for a head in the same launch (fc1_head)
-template <int KB, int MT, bool WT>
+template <int KB, int MT>
 __device__ __forceinline__ void fc1_fwd_body(const int w, const bf16* __restrict__ pool,
                                              const bf16* __restrict__ wf1,
                                              float* __restrict__ part, int B, int kchunk) {
@@ -409,56 +404,35 @@ __device__ __forceinline__ void fc1_fwd_body(const int w, const bf16* __restrict
       if (row < B) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          float* q = &out[(int64_t)row * HID + n0 + 16 * nt + rl];
-          if constexpr (WT) __hip_atomic_store(q, acc[mt][nt][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else st_ho<8>(q, acc[mt][nt][r]);
+          st_ho<8>(&out[(int64_t)row * HID + n0 + 16 * nt + rl], acc[mt][nt][r]);
         }
       }
     }
 }
 
-#endif  // PDM_WANT_FC1_FWD || PDM_WANT_FC1_HEAD
-#if PDM_WANT_FC1_FWD
 template <int KB, int MT = 1>
 __global__ __launch_bounds__(256, 2) void fc1_fwd_kernel(const bf16* __restrict__ pool,
                                                       const bf16* __restrict__ wf1,
                                                       float* __restrict__ part, int B, int kchunk) {
-  fc1_fwd_body<KB, MT, false>(blockIdx.x, pool, wf1, part, B, kchunk);
+  fc1_fwd_body<KB, MT>(blockIdx.x, pool, wf1, part, B, kchunk);
 }
 
 #endif  // PDM_WANT_FC1_FWD
-#if PDM_WANT_HEAD || PDM_WANT_FC1_HEAD
+#if PDM_WANT_HEAD
 // ---- head: fc1 reduce + bias + ReLU, fc2, CE, and (train) the head backward ----
 // One wave per batch row (HEAD_ROWS = 4 rows per workgroup, B/4 workgroups): lane j owns
 // hidden units 2j, 2j+1, so the fc2 logits are plain wave reductions and the split-K
 // partial loads of a row are spread over a whole wave.
 
-// a split-K partial pair: plain load, or (FUSED: written write-through by fc1_fwd workgroups of
-// the same launch) an sc1 load that bypasses this CU's L1 (MI355X_MICROARCH.md, visibility)
-template <bool FUSED>
-__device__ __forceinline__ float2 ld_part(const float* p) {
-  if constexpr (FUSED) {
-    const unsigned long long v = __hip_atomic_load(
-        reinterpret_cast<unsigned long long*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
-        __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_bit_cast(float2, v);
-  } else {
-    return *reinterpret_cast<const float2*>(p);
-  }
-}
-
-// workgroup blk of nblk (the head's grid, or the head part of fc1_head's).  FUSED: before the
-// first partial load, wait until `sync[0]` counts `nsplit` fc1_fwd workgroups (bounded: past
-// `timeout` ticks the error word sync[2] is set and the loss made NaN; fc1_head_kernel)
-template <bool TRAIN, bool FUSED>
+// workgroup blk of nblk (the head's grid)
+template <bool TRAIN>
 __device__ __forceinline__ void head_body(
     const int blk, const int nblk, const float* __restrict__ part, int S, int B,
     const float* __restrict__ bf1, const float* __restrict__ wf2, const float* __restrict__ bf2,
     const int32_t* __restrict__ ylab, bf16* __restrict__ dh, bf16* __restrict__ dht, int ldt,
     float* __restrict__ slab, double* __restrict__ metrics, int64_t* c0, int64_t* c1, unsigned* c2,
-    float* __restrict__ dh32, unsigned* sync, unsigned nsplit, long long timeout) {
+    float* __restrict__ dh32) {
   static_assert(HEAD_ROWS == 4, "one wave per row, 4 waves");
-  static_assert(!FUSED || TRAIN, "the fused head trains");
   __shared__ float hs[HEAD_ROWS][HID];
   __shared__ float dhs[HEAD_ROWS][HID];
   __shared__ float dls[HEAD_ROWS][NCLS];
@@ -477,22 +451,6 @@ __device__ __forceinline__ void head_body(
   float2 w2v[NCLS];
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) w2v[c] = reinterpret_cast<const float2*>(wf2 + c * HID)[j];
-  if constexpr (FUSED) {
-    // one lane polls the arrival count (sc1 loads, s_sleep) while the prologue loads above
-    // are in flight; the barrier then releases every wave to its partial loads
-    if (tid == 0) {
-      const long long deadline = (long long)__builtin_amdgcn_s_memrealtime() + timeout;
-      while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nsplit) {
-        if ((long long)__builtin_amdgcn_s_memrealtime() > deadline) {
-          atomicOr(sync + 2, 1u);
-          atomicAdd(&metrics[0], __builtin_nan(""));
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __syncthreads();
-  }
   for (int grp = blk; grp < ngroups; grp += nblk) {
     const int row = grp * HEAD_ROWS + r;
     const bool valid = row < B;
@@ -505,7 +463,7 @@ __device__ __forceinline__ void head_body(
       float2 u[32];
 #pragma unroll
       for (int q = 0; q < 32; ++q)
-        u[q] = ld_part<FUSED>(part + ((int64_t)q * B + rc) * HID + 2 * j);
+        u[q] = *reinterpret_cast<const float2*>(part + ((int64_t)q * B + rc) * HID + 2 * j);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
@@ -519,7 +477,8 @@ __device__ __forceinline__ void head_body(
         float2 u[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-          u[q] = ld_part<FUSED>(part + ((int64_t)min(s0 + q, S - 1) * B + rc) * HID + 2 * j);
+          u[q] = *reinterpret_cast<const float2*>(part + ((int64_t)min(s0 + q, S - 1) * B + rc) * HID +
+                                                  2 * j);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -625,61 +584,21 @@ __device__ __forceinline__ void head_body(
     if (c1) *c1 += 1;
     if (c2) *c2 += 1;
   }
-  if constexpr (FUSED) {
-    // the last head workgroup through re-arms the arrival count for the next launch (every
-    // fc1_fwd workgroup has arrived and every head workgroup has passed its wait)
-    if (tid == 0 && __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                        (unsigned)nblk - 1) {
-      __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   PDM_STAMP(15);
 }
 
-#endif  // PDM_WANT_HEAD || PDM_WANT_FC1_HEAD
-#if PDM_WANT_HEAD
+
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void cnn_head_kernel(
     const float* __restrict__ part, int S, int B, const float* __restrict__ bf1,
     const float* __restrict__ wf2, const float* __restrict__ bf2, const int32_t* __restrict__ ylab,
     bf16* __restrict__ dh, bf16* __restrict__ dht, int ldt, float* __restrict__ slab,
     double* __restrict__ metrics, int64_t* c0, int64_t* c1, unsigned* c2, float* __restrict__ dh32) {
-  head_body<TRAIN, false>(blockIdx.x, gridDim.x, part, S, B, bf1, wf2, bf2, ylab, dh, dht, ldt, slab,
-                          metrics, c0, c1, c2, dh32, nullptr, 0u, 0);
+  head_body<TRAIN>(blockIdx.x, gridDim.x, part, S, B, bf1, wf2, bf2, ylab, dh, dht, ldt, slab,
+                   metrics, c0, c1, c2, dh32);
 }
 
 #endif  // PDM_WANT_HEAD
-#if PDM_WANT_FC1_HEAD
-// ---- fc1_head: fc1_fwd and the training head in ONE launch (small and mid batches) ----
-// Workgroups [0, nsplit) are fc1_fwd's split-K workgroups: they store their partials
-// write-through, drain them (every wave: s_waitcnt vmcnt(0)), and one lane adds 1 to the
-// arrival count sync[0] behind a workgroup barrier.  The workgroups after them are the
-// head's: they issue their prologue loads (fc1 bias, fc2 weights), wait for the count to
-// reach nsplit, and read the partials with sc1 loads (MI355X_MICROARCH.md, visibility, first
-// row of the sc1 hand-off table).  What this saves over two launches is the boundary and
-// the head's own launch and prologue, which now run under the GEMM.  The launcher keeps the
-// grid within what the chip holds at once (fc1_fwd's 2 workgroups per CU), so a head
-// workgroup never waits for a split-K workgroup that could not be placed.
-template <int KB>
-__global__ __launch_bounds__(256, 2) void fc1_head_kernel(
-    const bf16* __restrict__ pool, const bf16* __restrict__ wf1, float* __restrict__ part, int B,
-    int kchunk, int nsplit, const float* __restrict__ bf1, const float* __restrict__ wf2,
-    const float* __restrict__ bf2, const int32_t* __restrict__ ylab, bf16* __restrict__ dh,
-    bf16* __restrict__ dht, int ldt, float* __restrict__ slab, double* __restrict__ metrics,
-    int64_t* c0, int64_t* c1, unsigned* c2, unsigned* sync, long long timeout) {
-  if ((int)blockIdx.x < nsplit) {
-    fc1_fwd_body<KB, 1, true>(blockIdx.x, pool, wf1, part, B, kchunk);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  head_body<true, true>(blockIdx.x - nsplit, gridDim.x - nsplit, part, FEAT / kchunk, B, bf1, wf2,
-                        bf2, ylab, dh, dht, ldt, slab, metrics, c0, c1, c2, nullptr, sync,
-                        (unsigned)nsplit, timeout);
-}
-#endif  // PDM_WANT_FC1_HEAD
 }  // namespace
 
 #if PDM_WANT_FWD_REST
@@ -736,29 +655,6 @@ void launch_cnn_head(const float* part, int splitk, int B, const float* bf1, con
 int cnn_head_blocks(int groups) { return groups < CNN_HEAD_MAX_BLOCKS ? groups : CNN_HEAD_MAX_BLOCKS; }
 
 #endif  // PDM_WANT_HEAD
-#if PDM_WANT_FC1_HEAD
-int fc1_head_grid(int B, int splitk, int ldt) {
-  if (B >= FC1_BIG_B || !(32 % splitk == 0 || 96 % splitk == 0)) return 0;
-  const int grid = ((B + 31) / 32) * splitk + cnn_head_blocks(ldt / HEAD_ROWS);
-  return grid <= FC1_HEAD_MAX_GRID ? grid : 0;
-}
-
-void launch_fc1_head(const __bf16* pool, const __bf16* wf1, float* part, int B, int splitk,
-                     const float* bf1, const float* wf2, const float* bf2, const int32_t* ylab,
-                     __bf16* dh, __bf16* dht, int ldt, float* slab, double* metrics, int64_t* c0,
-                     int64_t* c1, unsigned* c2, unsigned* sync, long long timeout, hipStream_t st) {
-  const int grid = fc1_head_grid(B, splitk, ldt);
-  const int nsplit = ((B + 31) / 32) * splitk;
-  if (32 % splitk == 0)
-    fc1_head_kernel<9><<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk, nsplit, bf1, wf2,
-                                             bf2, ylab, dh, dht, ldt, slab, metrics, c0, c1, c2,
-                                             sync, timeout);
-  else
-    fc1_head_kernel<3><<<grid, 256, 0, st>>>(pool, wf1, part, B, FEAT / splitk, nsplit, bf1, wf2,
-                                             bf2, ylab, dh, dht, ldt, slab, metrics, c0, c1, c2,
-                                             sync, timeout);
-}
-#endif  // PDM_WANT_FC1_HEAD
 #if PDM_WANT_FWD_REST
 #ifdef PDM_STAMPS
 void read_stamps_fwd(unsigned long long* host) {

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
   // 2. conv1 + bias + ReLU for a1 rows [d0, d0 + R + 2) (local rows 0 .. AR - 1)
   {
     const int rowg = IMG * (g < 3 ? g : 0);
-    const int a1c = ((((g >> 1) ^ (i16 & 3))) << 4) + 8 * (g & 1);
+    const int a1c = (conv1_pair_chunk(g) ^ (i16 & 3)) << 4;   // cnn_common.h conv1_pair
     bf16x4 bx[L::TPW1];
     int vv[L::TPW1];
 #pragma unroll
@@ -171,15 +171,16 @@ __global__ __launch_bounds__(FTH, 2) void cnn_fwd_band_kernel(
     for (int k = 0; k < L::TPW1; ++k) {
       const int y = vv[k] / IMG, x = vv[k] - y * IMG;
       const bool ok = y < L::AR && x < H1;
-      const int ab = (vv[k] - 2 * y) * 64 + a1c;
+      bf16x4 o[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w1f[mt], bx[k], b1v[mt], 0, 0, 0);
-        bf16x4 o = {to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
-                    to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
-        const int dst = ok ? L::A1 + (ab ^ (32 * mt)) : L::SPARE + lane * 8;
-        *reinterpret_cast<bf16x4*>(smem + dst) = o;
+        o[mt] = bf16x4{to_bf16(relu1(acc[0])), to_bf16(relu1(acc[1])),
+                       to_bf16(relu1(acc[2])), to_bf16(relu1(acc[3]))};
       }
+      // (dropped pixels: lane pairs share a 16-B slot of the 512-B spare area)
+      const int dst = ok ? L::A1 + (vv[k] - 2 * y) * 64 + a1c : L::SPARE + (lane & 31) * 16;
+      *reinterpret_cast<uint4*>(smem + dst) = conv1_pair(o[0], o[1]);
     }
   }
   if ((wave & 3) >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W2 DMA landed

@@ -97,11 +97,6 @@ __device__ __forceinline__ bool wait_peers(const XgmiArgs& a, int ph, int w, uns
 // BATCH: loads kept in flight per lane before their use (the persistent kernel uses 2 to
 // stay within the 32 registers per lane that cnn_bwd leaves free on a CU).  Indices are
 // 32-bit float4 counts (the host keeps every stage area below 2 GB).
-// PDM_XG_DIAG=1 (diagnostic builds, timing only, wrong results): no payload loads or stores,
-// only the flag protocol, to tell the data movement's cost from the hand-offs'.
-#ifndef PDM_XG_DIAG
-#define PDM_XG_DIAG 0
-#endif
 
 // U: float4 indices per thread per pass (U x BATCH loads in flight before their stores): the
 // loops are latency-bound (a 4.7 MB bucket at one load in flight per lane ran at ~0.2 TB/s
@@ -110,10 +105,6 @@ template <int BATCH, int U>
 __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsigned gen,
                                            long long deadline) {
   const int tid = threadIdx.x;
-  if (PDM_XG_DIAG == 1) {
-    signal_peers(a, 0, w, gen);
-    return wait_peers(a, 0, w, gen, deadline);
-  }
   const int N = a.nranks, r = a.rank;
   const f32x4* src = reinterpret_cast<const f32x4*>(a.src);
   const int n4 = (int)(a.n >> 2);
@@ -286,7 +277,18 @@ __global__ __launch_bounds__(64) void xgmi_wait_kernel(unsigned* loc, int signal
     if (!xg_wait_done(loc, c[i], m[i], timeout, /*acquire=*/false)) return;
 }
 
+// A bounded device stall for fault-injection tests: every wave reaches the exit once the
+// deadline passes.
+__global__ __launch_bounds__(64) void debug_spin_kernel(long long ticks) {
+  const long long end = (long long)__builtin_amdgcn_s_memrealtime() + ticks;
+  while ((long long)__builtin_amdgcn_s_memrealtime() < end) __builtin_amdgcn_s_sleep(64);
+}
+
 }  // namespace
+
+void launch_debug_spin(long long ticks, hipStream_t st) {
+  hipLaunchKernelGGL(debug_spin_kernel, dim3(1), dim3(64), 0, st, ticks);
+}
 
 void launch_xgmi_allreduce(const XgmiArgs& a, int nblk, hipStream_t st) {
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nblk), dim3(XG_THREADS), 0, st, a);

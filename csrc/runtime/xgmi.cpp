@@ -239,10 +239,31 @@ class XgmiReducer {
   void set_backward_channels(int n) {
     alive();
     TORCH_CHECK(n >= 1 && n <= (int)ch_.size(), "backward channels: 1..", ch_.size());
-    const unsigned v = (unsigned)n;
+    npub_ = (unsigned)n;
     XG_HIP_OK(hipSetDevice(device_));
-    XG_HIP_OK(hipMemcpy(static_cast<unsigned*>(local_) + XG_LOC_NPUB, &v, sizeof(v),
+    XG_HIP_OK(hipMemcpy(static_cast<unsigned*>(local_) + XG_LOC_NPUB, &npub_, sizeof(npub_),
                         hipMemcpyHostToDevice));
+  }
+
+  // Every protocol word back to its state after construction: this rank's heap (flags,
+  // stage rows, result arena) and local words (step / ready / done counters, call
+  // generations, error words).  The counters of a step structure that carried other
+  // channels in the persistent launch (with or without the in-launch exchange), or that
+  // stopped at a device deadline, no longer match what the next structure's kernels expect.
+  // Collective in effect: every rank resets between the same two control-plane agreements
+  // with every device drained, so no peer kernel writes into the zeroed heap and every
+  // rank's counters restart together (bench.py / parallel/startup.py candidate setup).
+  void reset() {
+    alive();
+    XG_HIP_OK(hipSetDevice(device_));
+    XG_HIP_OK(hipStreamSynchronize(stream_));
+    XG_HIP_OK(hipDeviceSynchronize());
+    XG_HIP_OK(hipMemset(heap_, 0, heap_bytes_));
+    XG_HIP_OK(hipMemset(local_, 0, XG_LOC_WORDS * sizeof(unsigned)));
+    XG_HIP_OK(hipMemcpy(static_cast<unsigned*>(local_) + XG_LOC_NPUB, &npub_, sizeof(npub_),
+                        hipMemcpyHostToDevice));
+    XG_HIP_OK(hipDeviceSynchronize());
+    pending_ = false;
   }
 
   at::Tensor sync() const {
@@ -383,6 +404,7 @@ class XgmiReducer {
   int64_t arena_ = 0;
   size_t result_off_ = 0, heap_bytes_ = 0;
   long long timeout_ticks_ = 0;
+  unsigned npub_ = 0;
   std::vector<Channel> ch_;
   Heap* heap_rec_ = nullptr;
   void* heap_ = nullptr;
@@ -417,6 +439,7 @@ void register_xgmi(py::module& m) {
       .def("end", &XgmiReducer::end)
       .def("sync", &XgmiReducer::sync)
       .def("set_backward_channels", &XgmiReducer::set_backward_channels)
+      .def("reset", &XgmiReducer::reset)
       .def("blocks", &XgmiReducer::blocks)
       .def("error", &XgmiReducer::error)
       .def("first_error", &XgmiReducer::first_error)

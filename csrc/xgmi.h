@@ -75,11 +75,9 @@ constexpr int XG_LOC_DONE = XG_LOC_ERR + 16;         // [XG_MAX_CH]
 constexpr int XG_LOC_LSTEP = XG_LOC_ERR + 64;        // [XG_MAX_WG] steps run by the streamed kernel
 constexpr int XG_LOC_XGEN = XG_LOC_LSTEP + XG_MAX_WG;  // [XG_XSLOTS] in-launch exchange calls
 constexpr int XG_LOC_WORDS = XG_LOC_XGEN + XG_XSLOTS;
-// workgroups of the persistent launch (PDM_XG_WG: diagnostic builds)
-#ifndef PDM_XG_WG
-#define PDM_XG_WG 64
-#endif
-constexpr int XG_STREAM_WG = PDM_XG_WG;
+// workgroups of the persistent launch (16 / 32 / 64 measured alike beside cnn_bwd once the
+// kernel used no LDS, profiles/r5/xgmi_width/)
+constexpr int XG_STREAM_WG = 64;
 static_assert(XG_STREAM_WG >= 1 && XG_STREAM_WG <= XG_MAX_WG, "persistent launch width");
 
 struct XgmiStreamArgs {
@@ -111,6 +109,9 @@ struct XgmiExch {
 // compute side of streamed mode: READY[signal_ch] = STEP, then wait DONE[ch[i]] >= mult[i]*STEP
 void launch_xgmi_wait(unsigned* loc, int signal_ch, int nwait, const int* ch, const unsigned* mult,
                       long long timeout, hipStream_t st);
+// fault injection (bench.py calibration tests): one wave that sleeps on the device for `ticks`
+// of s_memrealtime (100 MHz) and exits -- a bounded stand-in for a stuck kernel
+void launch_debug_spin(long long ticks, hipStream_t st);
 
 // Error bits of the rank's error word (XG_LOC_ERR).  A wait that runs past its deadline
 // records its own cause; a wait that gives up because the word was already set records

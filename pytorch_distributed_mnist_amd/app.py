@@ -88,6 +88,50 @@ def build_rank_state(args, rank: int, world_size: int, local_rank: int, init_pg:
     return ctx
 
 
+def structure_candidates(args, program, comm, world_size):
+    """[(name, apply, abortable)] in preference order for the start-up check
+    (parallel/startup.py); empty when there is nothing to choose or the check is off.
+    GPU with the direct xGMI transport: xgmi (conv bucket exchanged in the optimizer launch),
+    xgmi-noxchg (the exchange off), rccl-nocarry (plain RCCL collectives, built on demand).
+    abortable: a host deadline may abort the RCCL communicator (the xgmi kernels' waits are
+    bounded on the device: they end by themselves and report through the error word)."""
+    mode = getattr(args, "structure_check", "auto")
+    if mode == "off" or world_size < 2:
+        return []
+    red = program.reducer
+    spec = program.arena.spec
+    made = {}
+
+    def rebuilt(transport, **kw):
+        def apply():
+            if transport not in made:
+                made[transport] = parallel.GradReducer(comm, program.arena.grads,
+                                                       spec.bucket_bounds(), transport=transport,
+                                                       channels=spec.channel_bounds())
+            program.use_structure(made[transport], **kw)
+        return apply
+
+    cands = []
+    if red.kind == "xgmi":
+        cands.append(("xgmi", lambda: program.use_structure(red, xgmi_exchange=True), False))
+        if program.gpu is not None and hasattr(program.gpu, "xgmi_exchange") and \
+                program.structure.xgmi_exchange and red.exchange_ok(1):
+            cands.append(("xgmi-noxchg",
+                          lambda: program.use_structure(red, xgmi_exchange=False), False))
+        if isinstance(comm, parallel.RcclComm):
+            cands.append(("rccl-nocarry", rebuilt("rccl", rccl_mode="nocarry"), True))
+        elif mode == "on":
+            # the one-GPU rehearsal (xgmi over a gloo control plane): the gloo reducer
+            cands.append(("torch", rebuilt(None), True))
+    elif mode == "on":
+        # one structure: the check still runs when asked (the protocol's CPU / gloo
+        # rehearsal), with the same reducer rebuilt as the fallback
+        cands.append((red.kind, lambda: program.use_structure(red), True))
+        cands.append((f"{red.kind}-rebuilt", rebuilt(red.kind if red.kind != "torch" else None),
+                      True))
+    return cands if len(cands) > 1 else []
+
+
 def run(args):
     global best_acc
     launched = getattr(args, "_launched", False)
@@ -144,6 +188,7 @@ def run(args):
                                    transport=getattr(args, "comm", None),
                                    channels=spec.channel_bounds())
     dtype = resolve_dtype(args.dtype, args.arch, device)
+    reducer0 = reducer
     program = TrainProgram(args.arch, dtype, arena, optimizer, reducer, train_split, test_split,
                            args.batch_size, use_graphs=args.graphs)
     if device.type == "cuda":
@@ -159,6 +204,20 @@ def run(args):
     trainer = Trainer(program)
 
     try:
+        if not args.evaluate:
+            cands = structure_candidates(args, program, comm, world_size)
+            if cands:
+                from .parallel.startup import check_structures
+                idx = sampler.distributed_indices(len(train_split), world_size, rank,
+                                                  args.start_epoch)
+                if program.gpu is not None:
+                    idx = idx.to(torch.int32)
+
+                def check_sync(what, abortable):
+                    if device.type == "cuda":
+                        parallel.bounded_sync(device, args.timeout, comm, what, abort=abortable)
+                check_structures(program, cands, idx, rank, world_size, check_sync)
+        reducer = program.reducer          # (the start-up check may have switched it)
         if args.evaluate:
             test_loss, test_acc = trainer.evaluate()
             out('test loss: {}, test acc: {}.'.format(test_loss, test_acc))
@@ -213,7 +272,9 @@ def run(args):
             except RuntimeError:
                 if not pending:       # do not mask the error that is already propagating
                     raise
-        reducer.close()
+        program.reducer.close()
+        if program.reducer is not reducer0:
+            reducer0.close()
         comm.close()
         parallel.shutdown()
 

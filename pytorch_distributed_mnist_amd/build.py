@@ -68,12 +68,6 @@ def compile_flags(abi: int, inc):
         flags.append("-DPDM_DEBUG_BOUNDS=1")
     if knobs.get("PDM_STAMPS"):
         flags.append("-DPDM_STAMPS=1")
-    if knobs.get("PDM_DIAG_ROLES"):                   # fc1_bwd single-role launches
-        flags.append("-DPDM_DIAG_ROLES=1")
-    for k in ("PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL", "PDM_LIN_ROWS", "PDM_NT", "PDM_WT",
-              "PDM_XG_WG", "PDM_XG_DIAG", "PDM_FC1BWD_WPE", "PDM_DWC"):   # tuning experiments (diagnostic builds)
-        if os.environ.get(k):
-            flags.append(f"-D{k}={int(os.environ[k])}")
     if knobs.get("PDM_HIPCC_FLAGS"):                  # compiler experiments (diagnostic builds)
         flags += os.environ["PDM_HIPCC_FLAGS"].split()
     return flags
@@ -85,7 +79,6 @@ def compile_flags(abi: int, inc):
 # cnn_bwd (docs/kernels.md, tools/gpu_ab.sh).
 FILE_FLAGS = {
     "kernels/fc1_fwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-    "kernels/fc1_head.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "kernels/fc1_bwd.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "kernels/cnn_head.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
@@ -178,8 +171,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     # drop stale objects of sources that no longer exist / older hashes
     keep = set(objs)
     variant = custom_out or any(os.environ.get(k) for k in
-                                     ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_DIAG_ROLES", "PDM_DG_MTP", "PDM_DG_PFD", "PDM_ABL",
-                                      "PDM_LIN_ROWS", "PDM_NT", "PDM_HIPCC_FLAGS",
+                                     ("PDM_STAMPS", "PDM_DEBUG_BOUNDS", "PDM_HIPCC_FLAGS",
                                       "PDM_FILE_FLAGS"))
     for o in glob.glob(os.path.join(OBJ_DIR, "*.o")) if not variant else []:
         if o not in keep:

@@ -81,6 +81,12 @@ def build_parser() -> argparse.ArgumentParser:
                         'optimizer update over the ranks (reduce-scatter of its gradient, each '
                         'rank updates 128 / world_size rows, all-gather of the bf16 rows); '
                         'checkpoints gather the full state first and keep the reference format')
+    g.add_argument('--structure-check', choices=['auto', 'on', 'off'], default='auto',
+                   help='world size > 1: before the first epoch, run a few steps of each step '
+                        'structure in preference order and keep the first that passes on every '
+                        'rank, restoring the training state afterwards (auto: on the GPU when '
+                        'there is a fallback structure; on: also with a single structure, e.g. '
+                        'on CPU/gloo, where the fallback is the same reducer rebuilt)')
     g.add_argument('--checkpoint-dir', default='checkpoints')
     g.add_argument('--timeout', type=float, default=1800.0,
                    help='deadline in seconds for the rendezvous, RCCL communicator init and every '

@@ -17,7 +17,7 @@ from typing import Dict, Optional
 # experiments (timed runs leave them unset), "build" = extension build options.
 KNOBS: Dict[str, tuple] = {
     # step structure (bf16 CNN)
-    "PDM_RCCL_MODE": ("carry", "structure",
+    "PDM_RCCL_MODE": ("nocarry", "structure",
                       "RCCL step structure of the fc bucket: carry / nocarry / side / early / "
                       "zero (bench.py calibrates all of them when unset)"),
     "PDM_SHARD_FC": ("0", "structure", "1: shard the fc1 update over the ranks in bench.py"),
@@ -35,27 +35,21 @@ KNOBS: Dict[str, tuple] = {
     "PDM_FC1_CARRY_LOCAL": ("1", "structure", "0: world size 1 fuses the fc1 update into "
                             "fc1_bwd at every batch instead of carrying it into the next "
                             "forward launch where that is faster (B > 128)"),
-    "PDM_FUSE_HEAD": ("0", "structure", "1: fc1_fwd and the training head in one launch "
-                      "(fc1_head; measured slower, profiles/r5/fc1_head/)"),
     "PDM_BANDS": (None, "structure", "row bands per image in the conv backward (1 = off)"),
-    "PDM_FWD_BANDS": (None, "structure", "row bands of the forward alone"),
     "PDM_GRAPH_STEPS": ("8", "structure", "training steps per captured hipGraph (power of two)"),
-    "PDM_AHEAD_GATHER_WGS": ("0", "structure", "workgroups of the ahead-of-time epoch gather"),
     "PDM_FUSE_LIN_REDUCE": ("1", "structure", "0: separate lin_reduce at world size 1 (Linear)"),
-    "PDM_LIN_ROWS": (None, "diag", "rows per lin_train workgroup (kernel build constant)"),
     "PDM_F32_CONV": ("x3", "structure", "fp32 CNN conv2 products: x3 (split-bf16) / exact"),
     "PDM_F32_IPB": (None, "structure", "images per fp32 (exact) conv-backward workgroup"),
     "PDM_F32_UPW": (None, "structure", "(image, band) units per split-bf16 conv-backward workgroup"),
     # xGMI transport
     "PDM_XGMI_MODE": ("auto", "structure", "xgmi schedule: auto / one / two"),
     "PDM_XGMI_STREAM": ("1", "structure", "0: per-bucket xgmi launches, no persistent kernel"),
-    "PDM_XGMI_EARLY": ("1", "structure", "0: xgmi fc bucket after the conv backward"),
-    "PDM_XGMI_OPT_WAIT": ("0", "structure", "1: optimizer workgroups wait per bucket"),
     "PDM_XGMI_OUTSIDE": ("1", "structure", "0: the persistent xgmi collective inside every "
                          "step graph (fork / join edges) instead of launched per train_steps"),
     "PDM_XGMI_XCHG": ("1", "structure", "0: conv bucket via conv_reduce + the persistent "
                       "collective instead of the optimizer's in-launch exchange"),
-    "PDM_XGMI_TIMEOUT": ("60", "structure", "seconds any xgmi wait for a peer may take"),
+    "PDM_XGMI_TIMEOUT": ("30", "structure", "seconds any xgmi device wait for a peer may take "
+                         "(bench.py's calibration deadline is this plus PDM_CALIB_TIMEOUT_S)"),
     "PDM_XGMI_PROBE": ("1", "structure", "0: no child-process pre-flight of the xgmi "
                        "peer mappings before a rank maps them itself"),
     "PDM_XGMI_PROBE_TIMEOUT_S": ("120", "structure", "seconds the xgmi pre-flight may take"),
@@ -71,8 +65,9 @@ KNOBS: Dict[str, tuple] = {
     "PDM_CALIB_FAULT": (None, "diag", "fault injection into calibration: "
                         "<rank>:<candidate>:<setup|warm|timed|check|diverge|hang>[,...]"),
     "PDM_CALIB_BUDGET_S": ("120", "structure", "wall-clock budget (s) of bench.py's calibration"),
-    "PDM_CALIB_TIMEOUT_S": ("60", "structure", "deadline (s) of one calibration candidate's "
-                            "device sync (the run's --timeout if smaller)"),
+    "PDM_CALIB_TIMEOUT_S": ("30", "structure", "margin (s) of a calibration candidate's host "
+                            "deadline over the xgmi device timeout (the host waits strictly "
+                            "longer than any bounded device wait)"),
     "PDM_GATHER_AHEAD": ("1", "diag", "0: gather each epoch at its boundary"),
     # rehearsal / runtime
     "PDM_SHARE_DEVICE": ("0", "rehearsal", "1: every rank on device 0 (gloo / xgmi tests)"),
@@ -81,16 +76,6 @@ KNOBS: Dict[str, tuple] = {
     # extension build
     "PDM_DEBUG_BOUNDS": (None, "build", "device-side bounds checks"),
     "PDM_STAMPS": (None, "build", "s_memtime phase stamps (diagnostic build)"),
-    "PDM_DIAG_ROLES": (None, "build", "fc1_bwd single-role launches"),
-    "PDM_NT": (None, "build", "non-temporal slab stores / loads"),
-    "PDM_WT": (None, "build", "write-through hand-off store groups (bitmask, common.h st_ho)"),
-    "PDM_ABL": (None, "build", "timing ablations"),
-    "PDM_XG_WG": (None, "build", "workgroups of the persistent xgmi launch (diagnostic builds)"),
-    "PDM_XG_DIAG": (None, "build", "1: xgmi flag protocol without payload (timing only)"),
-    "PDM_FC1BWD_WPE": (None, "build", "fc1_bwd minimum waves per SIMD (launch bounds)"),
-    "PDM_DWC": (None, "build", "fc1_bwd weight-gradient batch rows per LDS round"),
-    "PDM_DG_MTP": (None, "build", "cnn_bwd dgrad tiles per pass"),
-    "PDM_DG_PFD": (None, "build", "cnn_bwd dgrad prefetch distance"),
     "PDM_HIPCC_FLAGS": (None, "build", "extra hipcc flags"),
     "PDM_FILE_FLAGS": (None, "build", "per-file hipcc flags"),
 }

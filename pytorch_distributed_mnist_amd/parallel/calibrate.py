@@ -116,14 +116,18 @@ class Calibration:
 
 def calibrate(cands: Sequence[Candidate], cp: ControlPlane, rank: int, *, warm_steps: int = 16,
               timed_steps: int = 48, rounds: int = 2, budget_s: float = 120.0,
-              inject: Optional[str] = None,
+              inject: Optional[str] = None, first_ok: bool = False,
               log: Callable[[str], None] = lambda s: None) -> Calibration:
     """Time every candidate (``rounds`` passes, alternate passes in reverse order to cancel
-    clock-ramp bias, the minimum per candidate) and return the agreed outcome."""
+    clock-ramp bias, the minimum per candidate) and return the agreed outcome.
+    ``first_ok``: a preference order instead -- stop at the first candidate that passes
+    (the app's start-up check, parallel/startup.py); ``best`` is that one."""
     res = Calibration()
     t_start = time.monotonic()
     alive = list(cands)
     for rnd in range(max(1, rounds)):
+        if first_ok and res.times:
+            break
         order = alive if rnd % 2 == 0 else list(reversed(alive))
         for c in order:
             if c.name in res.failed:
@@ -138,6 +142,8 @@ def calibrate(cands: Sequence[Candidate], cp: ControlPlane, rank: int, *, warm_s
             ms, why = _one(c, cp, rank, warm_steps, timed_steps, inject)
             if why is None:
                 res.times[c.name] = min(ms, res.times.get(c.name, math.inf))
+                if first_ok:
+                    break
                 continue
             res.failed[c.name] = why
             res.times.pop(c.name, None)
@@ -156,7 +162,7 @@ def calibrate(cands: Sequence[Candidate], cp: ControlPlane, rank: int, *, warm_s
         alive = [c for c in alive if c.name not in res.failed]
     if not res.times:
         raise RuntimeError("calibration: no step structure survived: " + "; ".join(res.notes))
-    res.best = min(res.times, key=res.times.get)
+    res.best = next(iter(res.times)) if first_ok else min(res.times, key=res.times.get)
     return res
 
 

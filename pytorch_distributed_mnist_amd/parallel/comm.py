@@ -108,14 +108,21 @@ class RcclComm(Communicator):
 
     def __init__(self, rank: int, world_size: int, device: torch.device, tag: str | None = None,
                  timeout_s: float = 1800.0):
-        C = _ext.require()
+        _ext.require()
         release_retired()
         self.rank, self.world_size = rank, world_size
         if tag is None:
             tag = str(next(_uid_counter))
-        key = f"pdm_amd/rccl_uid/{tag}"
-        dev = device.index if device.index is not None else torch.cuda.current_device()
+        self._tag = tag
+        self._gen = 0
+        self._dev = device.index if device.index is not None else torch.cuda.current_device()
         self.timeout_s = float(timeout_s)
+        self._c = None
+        self._create(f"pdm_amd/rccl_uid/{tag}")
+
+    def _create(self, key: str) -> None:
+        C = _ext.require()
+        rank, world_size, dev, timeout_s = self.rank, self.world_size, self._dev, self.timeout_s
         if world_size == 1:
             self._c = C.RcclComm(bytes(C.rccl_unique_id()), rank, 1, dev, float(timeout_s))
             return
@@ -153,6 +160,23 @@ class RcclComm(Communicator):
             except Exception:                  # noqa: BLE001 (the store may be gone too)
                 pass
             raise
+
+    @property
+    def alive(self) -> bool:
+        return self._c is not None
+
+    def revive(self) -> None:
+        """Replace this rank's communicator by a fresh one (a new unique id through the
+        rendezvous store).  Collective: every rank calls it, in the same order -- after a
+        deadline aborted the communicator on some rank (bounded_sync), the peers' communicators
+        are unusable too, so every rank drops its own (abort: its peers may be gone) and joins
+        the new one.  Native objects built on the old handle (GradReducer.rebind) must be
+        rebuilt by the caller."""
+        if self._c is not None:
+            self._c.abort()
+            self._c = None
+        self._gen += 1
+        self._create(f"pdm_amd/rccl_uid/{self._tag}/revive{self._gen}")
 
     @property
     def handle(self):
@@ -198,14 +222,19 @@ def _await_key(store, key: str, failed: str, timeout_s: float):
 
 
 def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | None = None,
-                 what: str = "device work") -> None:
+                 what: str = "device work", abort: bool = True) -> None:
     """``torch.cuda.synchronize`` with a deadline.
 
     Everything queued on the current stream (kernels, hipGraph replays, the RCCL
     collectives they wait on) must finish within ``timeout_s``; otherwise the RCCL
     communicator is aborted (its kernels waiting for a dead peer exit) and this raises.
     This is what bounds a collective that hangs on the device: the reference inherits
-    the same semantics from torch's NCCL watchdog (process-group timeout)."""
+    the same semantics from torch's NCCL watchdog (process-group timeout).
+
+    ``abort=False``: raise at the deadline but leave the communicator alone -- for work whose
+    every device wait is bounded by itself (the xGMI transport's kernels give up at their
+    own deadline and set an error word), so the device drains without an abort and the
+    communicator stays usable (bench.py's calibration of xgmi candidates)."""
     if device.type != "cuda":
         return
     ev = torch.cuda.Event()
@@ -215,10 +244,12 @@ def bounded_sync(device: torch.device, timeout_s: float, comm: Communicator | No
     while not ev.query():
         waited = time.monotonic() - t0
         if waited > timeout_s:
-            if isinstance(comm, RcclComm):
+            if abort and isinstance(comm, RcclComm):
                 comm.abort()
+                raise RuntimeError(f"{what} did not finish within {timeout_s:.0f} s (a peer rank "
+                                   f"is missing or hung); communicator aborted")
             raise RuntimeError(f"{what} did not finish within {timeout_s:.0f} s (a peer rank is "
-                               f"missing or hung); communicator aborted")
+                               f"missing or hung)")
         # spin for the first 50 ms (a timed window must not end with a sleep overshooting
         # the device by up to the backoff step), then back off to 1 ms polls
         if waited > 0.05:

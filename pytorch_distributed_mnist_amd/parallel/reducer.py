@@ -53,9 +53,11 @@ def default_transport() -> str:
 
 class GradReducer:
     def __init__(self, comm: Communicator, grads: torch.Tensor, bounds: List[Tuple[int, int]],
-                 force: bool = False, transport: str | None = None, channels=None):
+                 force: bool = False, transport: str | None = None, channels=None,
+                 timeout_s: float | None = None):
         """channels: (channel bounds, channel indices per bucket) -- the buckets cut further
-        for the direct xGMI transport (ModelSpec.channel_bounds); default one per bucket."""
+        for the direct xGMI transport (ModelSpec.channel_bounds); default one per bucket.
+        timeout_s: bound on every xgmi device wait for a peer (default PDM_XGMI_TIMEOUT)."""
         self.comm = comm
         self.grads = grads
         self.out_grads = grads          # what the optimizer reads after finalize()
@@ -80,7 +82,7 @@ class GradReducer:
         if grads.is_cuda and (transport == "xgmi" or
                               (transport == "auto" and isinstance(comm, RcclComm))):
             try:
-                x = XgmiTransport(comm, grads, self.cbounds)
+                x = XgmiTransport(comm, grads, self.cbounds, timeout_s=timeout_s)
                 x.native.set_backward_channels(len(self._bch[0]))
             except Exception as e:           # mapping or self-check failed on some rank
                 if transport == "xgmi":
@@ -101,6 +103,7 @@ class GradReducer:
             flat = [b for se in self.bounds for b in se]
             release_retired()
             self._native = C.GradReducer(comm.handle, grads, flat)
+            self._flat = flat
             self.kind = "rccl"
         else:
             self.kind = "torch" if isinstance(comm, TorchComm) else "local"
@@ -113,18 +116,59 @@ class GradReducer:
     def num_buckets(self) -> int:
         return len(self.bounds)
 
+    def rebind(self) -> None:
+        """RCCL: rebuild the native reducer on the communicator's current handle (after
+        RcclComm.revive replaced an aborted communicator); the bucket and shard setup is
+        re-applied.  Other transports hold no RCCL handle: nothing to do."""
+        if self.kind != "rccl":
+            return
+        C = _ext.require()
+        retire(self._native)
+        release_retired()
+        self._native = C.GradReducer(self.comm.handle, self.grads, self._flat)
+        if self.shard is not None:
+            self._native.set_shard(*self.shard)
+
+    def reset_transport(self) -> None:
+        """xgmi: every protocol word of this rank's transport back to its initial state
+        (XgmiReducer.reset: counters, generations, error words, the heap).  Needed whenever
+        the step structure on this transport changes (the persistent launch then carries other
+        channels, so the per-channel counters stop matching) or after a device deadline.  The
+        caller guarantees that every rank resets between the same two control-plane
+        agreements with its device drained (a candidate's setup phase).  No-op otherwise."""
+        if self.kind == "xgmi":
+            self._native.reset()
+
+    def exchange_ok(self, bucket: int) -> bool:
+        """xgmi: bucket `bucket` can be all-reduced inside the optimizer launch (its channels
+        are one-shot; XgmiReducer.fill_exchange refuses a two-shot one, e.g. PDM_XGMI_MODE=two)."""
+        if self.kind != "xgmi":
+            return False
+        desc = self._xgmi.describe
+        return all(desc[c]["mode"] == "one-shot" for c in self._bch[bucket])
+
     # -- xgmi streamed mode -------------------------------------------------------
     def begin(self, nsteps: int, nch: int | None = None, wide: bool = False) -> None:
         """Launch the persistent collective for the next ``nsteps`` steps, carrying the first
         ``nch`` buckets (default: all; the others are exchanged in-launch by their producer,
         ``launch_optimizer(exchange=True)``); `wide`: the variant with twice the loads in
         flight, which fits only beside the small-band backward kernels."""
+        if self.fault_no_collective:
+            return
         n = -1 if nch is None else sum(len(self._bch[b]) for b in range(int(nch)))
         self._native.begin(nsteps, n, bool(wide))
 
     def end(self) -> None:
         """Join the persistent collective back into the compute stream."""
+        if self.fault_no_collective:
+            return
         self._native.end()
+
+    # fault injection (bench.py PDM_CALIB_FAULT "<rank>:<xgmi candidate>:devhang"): this rank
+    # never launches its persistent collective, so its buckets are never pushed to the peers
+    # and its own optimizer's waits for reduced buckets are never satisfied -- a real device
+    # hang on every rank, which the bounded device waits turn into error words
+    fault_no_collective = False
 
     def bucket_of(self, offset: int) -> int:
         for i, (s, e) in enumerate(self.bounds):
@@ -282,7 +326,7 @@ class XgmiTransport:
         dev = grads.device.index or 0
         mode = mode or knobs.get("PDM_XGMI_MODE", "auto")
         # bound on any wait for a peer inside the kernel (a late peer is an error, not a hang)
-        timeout_s = timeout_s or float(knobs.get("PDM_XGMI_TIMEOUT", "60"))
+        timeout_s = timeout_s or float(knobs.get("PDM_XGMI_TIMEOUT", "30"))
         flat = [b for se in bounds for b in se]
         err = None
         native = None

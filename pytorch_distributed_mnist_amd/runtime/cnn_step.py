@@ -94,16 +94,6 @@ def choose_bands(B: int, cus: int = 256, forced=None) -> int:
     return 1
 
 
-def choose_fwd_bands(B: int, forced=None, bands_forced=None) -> int:
-    """Row bands per image in the forward: the backward's split (the band backward reads the
-    band forward's a1 / normalised x); `forced` (StepStructure.fwd_bands / PDM_FWD_BANDS)
-    splits the forward alone (it then hands the one-image backward the uint8 image, as
-    cnn_fwd does)."""
-    if forced is not None and choose_bands(B, forced=bands_forced) == 1:
-        return int(forced)
-    return choose_bands(B, forced=bands_forced)
-
-
 def conv_blocks(C, B: int, bands_forced=None) -> int:
     """Conv-backward workgroups (= gradient slabs) for per-rank batch B."""
     bands = choose_bands(B, forced=bands_forced)
@@ -132,8 +122,6 @@ class CnnStep(GpuStepBase):
         self.dht = torch.zeros(self.ldt * 128, dtype=bf16, device=dev)
         self.head_slab = torch.empty(C.cnn_head_nblk(self.ldt) * C.CNN_HEAD_SLAB, dtype=torch.float32,
                                      device=dev)
-        # fc1_head's arrival count / head passes / error bit (the kernel re-arms the first two)
-        self.fc1_head_sync = torch.zeros(4, dtype=torch.int32, device=dev)
         self.dpool = torch.empty(B * 9216, dtype=bf16, device=dev)
         self.ipb = choose_ipb(B)
         # row-band steps (small batches): the forward hands a1 and the normalised x to the
@@ -200,6 +188,9 @@ class CnnStep(GpuStepBase):
         # all-gathered; W1^T is re-derived locally.  Same arithmetic per element as the
         # replicated update; the fp32 rows a rank does not own go stale until sync_master()
         # (checkpoints, evaluation of the fp32 weights, parameter checks)
+        # xgmi streamed: the conv bucket all-reduced inside the optimizer launch
+        # (StepStructure.xgmi_exchange; bench.py's 'xgmi-noxchg' candidate turns it off)
+        self.xgmi_exchange = st.xgmi_exchange
         self.shard_fc = False
         self._shard_rows = None
         self._side = None
@@ -400,8 +391,7 @@ class CnnStep(GpuStepBase):
         train_steps call keeps the fused update."""
         st = self.structure
         return (not self.reducer.active and self.fuse_fc1 and st.fc1_carry_fwd and
-                st.fc1_carry_local and self.bands(B) == 1 and
-                choose_fwd_bands(B, st.fwd_bands, st.bands) == 1)
+                st.fc1_carry_local and self.bands(B) == 1)
 
     def _fwd_carry_on(self, B: int) -> bool:
         """SGD: step k's fc1 update runs in step k+1's forward launch (kernels/fc_carry.h) --
@@ -435,9 +425,8 @@ class CnnStep(GpuStepBase):
     def fwd_outputs(self, B: int):
         """cnn_fwd's training outputs for per-rank batch B: (xg, ylab, bands, a1g, xng) -- the
         band backward reads a1 + normalised x, the one-image backward the uint8 image."""
-        st = self.structure
-        fb = choose_fwd_bands(B, st.fwd_bands, st.bands)
-        if self.bands(B) > 1:
+        fb = self.bands(B)
+        if fb > 1:
             return None, self.ylab, fb, self.a1g, self.xng
         return self.xg, self.ylab, fb, None, None
 
@@ -477,18 +466,6 @@ class CnnStep(GpuStepBase):
         if streamed:
             self.reducer.end()
 
-    def fused_head(self, B: int) -> bool:
-        """fc1_fwd and the head as one launch (fc1_head) for per-rank batch B."""
-        return (self.structure.fuse_head and
-                self.C.fc1_head_grid(B, self.splitk_train, -(-B // 32) * 32) > 0)
-
-    def check_device(self) -> None:
-        """Raise if a fused fc1_head launch gave up waiting for its split-K workgroups (its
-        head then ran on incomplete partials and made the train loss NaN)."""
-        if int(self.fc1_head_sync[2].item()) != 0:
-            raise RuntimeError("fc1_head: a head workgroup timed out waiting for the split-K "
-                               "workgroups of its launch; this run's results are invalid")
-
     def _train_impl(self, B: int, carry_in: bool = False, carry_out: bool = False,
                     fwd_in: bool = False, fwd_out: bool = False) -> None:
         """One training step (kernel chain in the module docstring).
@@ -518,16 +495,10 @@ class CnnStep(GpuStepBase):
         elif carry_in:
             self.reducer.wait_bucket(0)
             self.launch_optimizer(self._bucket_segments()[0])
-        if self.fused_head(B):
-            C.fc1_head(self.pool, self.wf1, self.part, B, S, P["fc1.bias"], P["fc2.weight"],
-                       P["fc2.bias"], self.ylab, self.dh, self.dht, ldt, self.head_slab,
-                       self.metrics.train_view(), self.ctr[0:1], self.opt._step_dev,
-                       self.fc1_head_sync, xs)
-        else:
-            C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
-            C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
-                       True, self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
-                       self.ctr[0:1], self.opt._step_dev, xs)
+        C.fc1_fwd(self.pool, self.wf1, self.part, B, S)
+        C.cnn_head(self.part, S, B, P["fc1.bias"], P["fc2.weight"], P["fc2.bias"], self.ylab,
+                   True, self.dh, self.dht, ldt, self.head_slab, self.metrics.train_view(),
+                   self.ctr[0:1], self.opt._step_dev, xs)
         C.fc1_bwd(self.dh, self.dht, ldt, self.pool, self.current_wf1t(), B, G["fc1.weight"], self.dpool,
                   self.head_slab, G["fc2.weight"], G["fc2.bias"], G["fc1.bias"],
                   self.metrics.train_view(),
@@ -648,10 +619,12 @@ class CnnStep(GpuStepBase):
             self.launch_optimizer(b0)
 
     def _xchg(self) -> bool:
-        """xgmi streamed mode with the conv bucket exchanged inside the optimizer launch."""
+        """xgmi streamed mode with the conv bucket exchanged inside the optimizer launch (a
+        one-shot conv channel only: PDM_XGMI_MODE=two falls back to conv_reduce + the
+        persistent collective)."""
         red = self.reducer
         return (red.active and getattr(red, "kind", None) == "xgmi" and red.streamed and
-                self.structure.xgmi_exchange)
+                self.xgmi_exchange and red.exchange_ok(1))
 
     def _fc_update(self, store_grad: bool = False):
         """fc1_bwd's fused fc1-weight SGD update (bind.cpp make_fc_update); store_grad: store

@@ -123,15 +123,13 @@ class GpuStepBase:
         returns the event behind it."""
         n = self._n_epoch
         buf = self._stage(idx)
-        cur_stream = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(stream):
             self.C.gather_epoch(self.train_images, self.train_labels, buf[0],
                                 self.ep_images.view(-1, 784)[half * n:(half + 1) * n],
                                 self.ep_labels[half * n:(half + 1) * n],
-                                # workgroups of the ahead-of-time gather beside the steps
-                                # (0: one per 16 rows; grid-striding ones take fewer CUs)
-                                max_wgs=0 if stream is cur_stream else
-                                self.structure.ahead_gather_wgs)
+                                # one workgroup per 16 rows (grid-striding ones taking
+                                # fewer CUs beside the steps measured no better)
+                                max_wgs=0)
             ev = torch.cuda.Event()
             ev.record(stream)
         buf[1] = ev
@@ -372,11 +370,10 @@ class GpuStepBase:
         """One fused optimizer launch over `segments` (default: every parameter).
 
         xgmi streamed mode: bucket `signal_ch` (>= 0) is published to the persistent
-        collective and the update waits for the buckets its segments belong to — by a
-        one-workgroup wait kernel in front of it (default), or, with
-        PDM_XGMI_OPT_WAIT=1, by every optimizer workgroup for its own segment's bucket
-        (lets the fc update run while the conv bucket is still in flight, but parks the
-        optimizer's whole grid on the GPU meanwhile).
+        collective and the update waits for the buckets its segments belong to, by a
+        one-workgroup wait kernel in front of it (every optimizer workgroup waiting for its
+        own segment's bucket parked the whole grid on the GPU meanwhile; that variant was
+        measured slower and removed in round 6).
         """
         if self._opt_segments is None:
             self._opt_segments = self.optimizer_segments()
@@ -392,14 +389,11 @@ class GpuStepBase:
                       xchg_bucket=red.channels_of(1)[0])
         elif red.streamed:
             waits = red.waits_for(segs)
-            if self.structure.xgmi_opt_wait:
-                xg = dict(xg=red.sync, signal_ch=signal_ch, waits=waits, timeout_s=red.timeout_s)
-            else:
-                uniq = []
-                for i in range(0, len(waits), 2):
-                    if waits[i] not in uniq[0::2]:
-                        uniq += waits[i:i + 2]
-                self.C.xgmi_wait(red.sync, signal_ch, uniq, red.timeout_s)
+            uniq = []
+            for i in range(0, len(waits), 2):
+                if waits[i] not in uniq[0::2]:
+                    uniq += waits[i:i + 2]
+            self.C.xgmi_wait(red.sync, signal_ch, uniq, red.timeout_s)
         o = self.opt
         g = o.param_groups[0]
         grads = self.reducer.out_grads       # the xgmi transport's result arena, or in place

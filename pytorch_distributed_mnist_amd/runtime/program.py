@@ -43,6 +43,7 @@ class TrainProgram:
         if self.batch_size < 1:
             raise ValueError("per-rank batch size must be >= 1")
         self.eval_batch = int(eval_batch or self.batch_size)
+        self.use_graphs = bool(use_graphs)
         self.metrics = DeviceMetrics(self.device)
         self.is_gpu = self.device.type == "cuda"
         self.train_split = train_split
@@ -149,6 +150,25 @@ class TrainProgram:
             n = count * self.reducer.comm.world_size
             for buf in self.optimizer.state_buffers().values():
                 self.reducer.gather(buf[start:start + n])
+
+    def use_structure(self, reducer, rccl_mode: Optional[str] = None,
+                      xgmi_exchange: Optional[bool] = None) -> None:
+        """Switch the step to another gradient reducer and step structure (the start-up
+        check's fallbacks, parallel/startup.py; bench.py's calibration candidates): graphs
+        are re-captured on next use."""
+        self.reducer = reducer
+        g = self.gpu
+        if g is None:
+            return
+        if getattr(g, "shard_fc", False):
+            g.set_shard_fc(False)            # (gathers the sharded state on the old reducer)
+        g.reducer = reducer
+        g.use_graphs = self.use_graphs and reducer.capturable
+        if rccl_mode is not None and hasattr(g, "set_rccl_mode"):
+            g.set_rccl_mode(rccl_mode, invalidate=False)
+        if xgmi_exchange is not None and hasattr(g, "xgmi_exchange"):
+            g.xgmi_exchange = bool(xgmi_exchange) and self.structure.xgmi_exchange
+        g.invalidate_graphs()
 
     def run_steps(self, n: int, bsz: Optional[int] = None) -> None:
         """Run ``n`` full steps from the current counter (bench helper; GPU only)."""

@@ -19,8 +19,11 @@ RCCL_MODES = ("carry", "nocarry", "side", "early", "zero")
 
 @dataclass(frozen=True)
 class StepStructure:
-    # RCCL data plane: placement of the fc bucket's all-reduce and update (cnn_step.CnnStep)
-    rccl_mode: str = "carry"
+    # RCCL data plane: placement of the fc bucket's all-reduce and update (cnn_step.CnnStep):
+    # nocarry (one grouped launch, the fc1 update carried into the next forward) is the
+    # fastest RCCL structure in every N = 1 calibration (profiles/r5/final4/bench.jsonl:
+    # 57.1 vs 62.3 us for carry at B = 256, 41.7 vs 46.6 at B = 32)
+    rccl_mode: str = "nocarry"
     # largest fc1_fwd split-K factor
     splitk_cap: int = 32
     # world size > 1, SGD (the xgmi in-launch-exchange and RCCL nocarry steps): step k's fc1
@@ -34,11 +37,6 @@ class StepStructure:
     # of fusing it into fc1_bwd's weight-gradient tiles, at the batches CnnStep._local_carry
     # names (fc1_bwd then stores the gradient; a call's last step still fuses its update)
     fc1_carry_local: bool = True
-    # training: fc1_fwd and the head in one launch (fc1_head) where the grid allows it.  Off:
-    # measured slower than the two launches (B = 256: 60.1-61.2 vs 53.1-53.7 us per step;
-    # B = 32: 38.9 vs 37.4-37.7; profiles/r5/fc1_head/) -- the write-through partials and
-    # the in-launch wait cost more than the kernel boundary they replace
-    fuse_head: bool = False
     # world size 1: the conv slab reduction inside the optimizer launch
     fuse_conv_reduce: bool = True
     # world size 1, SGD: fc1's update in fc1_bwd's weight-gradient tiles
@@ -47,12 +45,10 @@ class StepStructure:
     fc1_wt_double: bool = True
     # store the fc1 weight gradient the fused update consumes (tests / diagnostics)
     keep_grads: bool = False
-    # row bands per image of the conv backward / of the forward alone (None = by batch)
+    # row bands per image of the conv forward and backward (None = by batch)
     bands: Optional[int] = None
-    fwd_bands: Optional[int] = None
-    # xgmi: the fc bucket leaves right after fc1_bwd; optimizer workgroups wait per bucket
+    # xgmi (per-bucket launches, PDM_XGMI_STREAM=0): the fc bucket leaves right after fc1_bwd
     xgmi_early: bool = True
-    xgmi_opt_wait: bool = False
     # xgmi streamed (CNN): the conv bucket all-reduced inside the optimizer launch that
     # reduces its slabs (no conv_reduce launch, no wait launch); False: conv_reduce, the
     # persistent collective, a wait launch
@@ -62,8 +58,6 @@ class StepStructure:
     xgmi_outside: bool = True
     # Linear, world size 1: the slab reduction inside the optimizer launch
     fuse_lin_reduce: bool = True
-    # workgroups of the ahead-of-time epoch gather (0: one per 16 rows)
-    ahead_gather_wgs: int = 0
     # fp32 CNN: conv2 / fc1 products ("x3" split-bf16, "exact" fp32 MFMA); conv-backward
     # work per workgroup (None = by batch): (image, band) units (x3) / images (exact)
     f32_conv: str = "x3"
@@ -94,7 +88,6 @@ class StepStructure:
         d = cls()
         return cls(rccl_mode=knobs.get("PDM_RCCL_MODE", d.rccl_mode),
                    splitk_cap=int(knobs.get("PDM_SPLITK_CAP", str(d.splitk_cap))),
-                   fuse_head=flag("PDM_FUSE_HEAD", d.fuse_head),
                    fc1_carry_fwd=flag("PDM_FC1_CARRY_FWD", d.fc1_carry_fwd),
                    fc1_carry_graphs=flag("PDM_FC1_CARRY_GRAPHS", d.fc1_carry_graphs),
                    fc1_carry_local=flag("PDM_FC1_CARRY_LOCAL", d.fc1_carry_local),
@@ -102,9 +95,7 @@ class StepStructure:
                    fuse_fc1=flag("PDM_FUSE_FC1", d.fuse_fc1),
                    fc1_wt_double=flag("PDM_FC1_WT2", d.fc1_wt_double),
                    keep_grads=knobs.get("PDM_KEEP_GRADS", "0") == "1",
-                   bands=opt_int("PDM_BANDS"), fwd_bands=opt_int("PDM_FWD_BANDS"),
-                   xgmi_early=flag("PDM_XGMI_EARLY", d.xgmi_early),
-                   xgmi_opt_wait=knobs.get("PDM_XGMI_OPT_WAIT", "0") == "1",
+                   bands=opt_int("PDM_BANDS"),
                    # ranks sharing one GPU (the one-GPU rehearsal): the exchange's spinning
                    # optimizer grid would keep a peer's cnn_bwd, which needs a whole CU, off
                    # the device until the wait times out -- the wait launch is used there
@@ -112,7 +103,6 @@ class StepStructure:
                    xgmi_exchange=flag("PDM_XGMI_XCHG", d.xgmi_exchange) and
                    knobs.get("PDM_SHARE_DEVICE") != "1",
                    fuse_lin_reduce=flag("PDM_FUSE_LIN_REDUCE", d.fuse_lin_reduce),
-                   ahead_gather_wgs=int(knobs.get("PDM_AHEAD_GATHER_WGS", "0")),
                    f32_conv=knobs.get("PDM_F32_CONV", d.f32_conv),
                    f32_upw=opt_int("PDM_F32_UPW"), f32_ipb=opt_int("PDM_F32_IPB"),
                    emulate_ws=opt_int("PDM_EMULATE_WS"))

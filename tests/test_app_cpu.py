@@ -150,3 +150,32 @@ def test_cnn_sharded_fc1_update_matches_replicated_cpu(tmp_path):
     out = run_cli(["--arch", "cnn", "--optimizer", "sgd", "--evaluate", "--resume",
                    str(d2 / "checkpoints" / "checkpoint_0.pth.tar")], d2)
     assert re.search(r"^test loss: \d+\.\d{6}, test acc: \d+\.\d{2}%\.$", out, re.M)
+
+
+def test_structure_check_falls_back_with_identical_epoch_lines(tmp_path):
+    """The start-up structure check on CPU/gloo, two ranks (parallel/startup.py): the first
+    structure fails on rank 1 (an injected fault in its check phase), every rank drops it and
+    keeps the fallback, with a warning on stderr; the training state the check changed is
+    restored, so the epoch lines equal those of a run without the check."""
+    d1, d2 = tmp_path / "off", tmp_path / "on"
+    d1.mkdir()
+    d2.mkdir()
+    common = ["--epochs", "2", "--synthetic-size", "2048", "--seed", "5", "--arch", "cnn",
+              "--optimizer", "sgd", "--lr", "0.05", "--world-size", "2"]
+    ref = run_cli(common + ["--structure-check", "off"], d1)
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               PDM_CALIB_FAULT="1:torch:check")
+    cmd = [sys.executable, os.path.join(REPO, "multi_proc_single_gpu.py"), "--device", "cpu",
+           "--backend", "gloo", "-i", f"tcp://127.0.0.1:{free_port()}", "--synthetic"] + \
+        common + ["--structure-check", "on"]
+    r = subprocess.run(cmd, cwd=d2, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "torch failed calibration: check on rank 1" in r.stderr, r.stderr
+    assert "using step structure 'torch-rebuilt' instead of 'torch'" in r.stderr, r.stderr
+    # (each rank prints its own epoch lines, in either order)
+    ep = lambda out: sorted(l for l in out.splitlines() if l.startswith("Epoch:"))
+    assert len(ep(ref)) == 4 and ep(r.stdout) == ep(ref)
+    a = torch.load(d1 / "checkpoints" / "checkpoint_1.pth.tar", weights_only=True)
+    b = torch.load(d2 / "checkpoints" / "checkpoint_1.pth.tar", weights_only=True)
+    for k, v in a["state_dict"].items():
+        assert torch.equal(v, b["state_dict"][k]), k

@@ -88,7 +88,7 @@ def test_calibration_drops_candidates_failing_on_one_rank():
     """Each kind of failure on ONE rank (an exception in setup / timed steps, a device sync
     that hits its deadline, replicas that drift apart) drops that candidate on EVERY rank,
     with the reason recorded; the fastest survivor is chosen and one JSON line printed."""
-    faults = "1:rccl-early:timed,0:rccl:diverge,1:xgmi:hang,0:rccl-side:setup"
+    faults = "1:rccl-early:timed,0:rccl:diverge,1:xgmi:hang,0:xgmi-noxchg:setup"
     d = _line(_run(["--gpus", "2", "--dry-run"], env={"PDM_CALIB_FAULT": faults}))
     assert d["config"]["grad_transport"] == "rccl-nocarry"
     assert list(d["config"]["transport_calibration_ms_per_step"]) == ["rccl-nocarry"]
@@ -96,7 +96,7 @@ def test_calibration_drops_candidates_failing_on_one_rank():
     for what in ("rccl-early failed calibration: timed on rank 1",
                  "rccl failed calibration: replicas diverged",
                  "xgmi failed calibration: warm on rank 1",
-                 "rccl-side failed calibration: setup on rank 0"):
+                 "xgmi-noxchg failed calibration: setup on rank 0"):
         assert what in notes, notes
 
 
@@ -107,20 +107,58 @@ def test_calibration_failure_in_check_phase_four_ranks():
 
 
 def test_calibration_with_no_survivor_is_fatal():
-    faults = ",".join(f"1:{n}:setup" for n in ("xgmi", "rccl", "rccl-nocarry", "rccl-side",
+    faults = ",".join(f"1:{n}:setup" for n in ("xgmi", "xgmi-noxchg", "rccl", "rccl-nocarry",
                                                  "rccl-early"))
     r = _run(["--gpus", "2", "--dry-run"], env={"PDM_CALIB_FAULT": faults})
     assert r.returncode != 0
     assert "no step structure survived" in r.stderr
 
 
-def test_zero_is_never_an_automatic_candidate(monkeypatch):
+class _Red:
+    """A stand-in reducer for step_candidates (xgmi: whether the conv bucket is one-shot)."""
+    def __init__(self, one_shot=True):
+        self.one_shot = one_shot
+
+    def exchange_ok(self, bucket):
+        return self.one_shot
+
+
+def test_candidates_at_most_four_per_batch(monkeypatch):
+    """The automatic calibration list: at most four structures per batch, each with its N>1
+    argument (bench.step_candidates); 'side' and 'zero' only when forced."""
     b = _bench()
-    reds = {"xgmi": object(), "rccl": object()}
     monkeypatch.delenv("PDM_RCCL_MODE", raising=False)
-    names = [c[0] for c in b.step_candidates(reds, "cnn", lambda r: True)]
-    assert names == ["xgmi", "rccl", "rccl-nocarry", "rccl-side", "rccl-early"]
+    reds = {"xgmi": _Red(), "rccl": _Red()}
+    big = [c[0] for c in b.step_candidates(reds, "cnn", 256, lambda r: True)]
+    small = [c[0] for c in b.step_candidates(reds, "cnn", 32, lambda r: True)]
+    assert big == ["xgmi", "xgmi-noxchg", "rccl-nocarry", "rccl"]
+    assert small == ["xgmi", "xgmi-noxchg", "rccl-nocarry", "rccl-early"]
+    # the xgmi fallback without the in-launch exchange is a distinct structure only when the
+    # exchange is possible (one-shot conv channel) and on (StepStructure.xgmi_exchange)
+    reds2 = {"xgmi": _Red(one_shot=False), "rccl": _Red()}
+    assert [c[0] for c in b.step_candidates(reds2, "cnn", 256, lambda r: True)] == \
+        ["xgmi", "rccl-nocarry", "rccl"]
+    assert [c[0] for c in b.step_candidates(reds, "cnn", 256, lambda r: True,
+                                            exchange_step=False)] == \
+        ["xgmi", "rccl-nocarry", "rccl"]
+    flags = {c[0]: c[3] for c in b.step_candidates(reds, "cnn", 256, lambda r: True)}
+    assert flags["xgmi"] is True and flags["xgmi-noxchg"] is False
+    # the gloo rehearsal's reducer is a candidate of its own
+    assert [c[0] for c in b.step_candidates({"xgmi": _Red(), "torch": _Red()}, "cnn", 256,
+                                            lambda r: True)] == ["xgmi", "xgmi-noxchg", "torch"]
+
+
+def test_zero_and_side_are_never_automatic_candidates(monkeypatch):
+    b = _bench()
+    reds = {"xgmi": _Red(), "rccl": _Red()}
+    monkeypatch.delenv("PDM_RCCL_MODE", raising=False)
+    names = [c[0] for c in b.step_candidates(reds, "cnn", 256, lambda r: True)]
+    assert "rccl-zero" not in names and "rccl-side" not in names
     monkeypatch.setenv("PDM_RCCL_MODE", "zero")
-    assert [c[0] for c in b.step_candidates(reds, "cnn", lambda r: True)] == ["xgmi", "rccl-zero"]
-    monkeypatch.setenv("PDM_RCCL_MODE", "early")
-    assert [c[0] for c in b.step_candidates(reds, "cnn", lambda r: True)] == ["xgmi", "rccl-early"]
+    assert [c[0] for c in b.step_candidates(reds, "cnn", 256, lambda r: True)] == \
+        ["xgmi", "xgmi-noxchg", "rccl-zero"]
+    assert [c[0] for c in b.step_candidates(reds, "cnn", 256, lambda r: False)] == \
+        ["xgmi", "xgmi-noxchg"]
+    monkeypatch.setenv("PDM_RCCL_MODE", "side")
+    assert [c[0] for c in b.step_candidates(reds, "cnn", 32, lambda r: True)] == \
+        ["xgmi", "xgmi-noxchg", "rccl-side"]

@@ -132,3 +132,32 @@ def test_cnn_fp32_cli_train_resume_evaluate_matches_cpu(gpu, tmp_path, monkeypat
                          "--synthetic-size", "2048", "--epochs", "3", "--resume", str(ck)], d1)
          if l.startswith("Epoch:")]
     assert len(r) == 1 and r[0].startswith("Epoch: 2/3,")
+
+
+def test_structure_check_falls_back_after_xgmi_device_hang(gpu, tmp_path, monkeypatch):
+    """The app's start-up structure check (parallel/startup.py) on two ranks sharing the GPU:
+    the direct xGMI transport is the first structure, and rank 1 never launches its
+    persistent collective (PDM_CALIB_FAULT devhang) -- a real device hang that the xgmi
+    kernels' bounded waits end after PDM_XGMI_TIMEOUT.  Every rank drops xgmi (error word),
+    restores the training state and runs on the gloo reducer, with a warning; the epoch lines
+    equal those of a run on the gloo reducer without any check."""
+    monkeypatch.setenv("PDM_SHARE_DEVICE", "1")
+    d1, d2 = tmp_path / "plain", tmp_path / "checked"
+    d1.mkdir()
+    d2.mkdir()
+    common = ["--arch", "cnn", "--optimizer", "sgd", "--lr", "0.05", "--synthetic-size", "2048",
+              "--epochs", "2", "--seed", "9", "--world-size", "2"]
+    ref = cli(common + ["--structure-check", "off"], d1, backend="gloo")
+    monkeypatch.setenv("PDM_XGMI_TIMEOUT", "3")
+    monkeypatch.setenv("PDM_CALIB_FAULT", "1:xgmi:devhang")
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, os.path.join(REPO, "multi_proc_single_gpu.py"), "--device", "cuda",
+           "--backend", "gloo", "-i", f"tcp://127.0.0.1:{free_port()}", "--synthetic"] + \
+        common + ["--comm", "xgmi", "--structure-check", "on"]
+    r = subprocess.run(cmd, cwd=d2, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "xgmi failed calibration" in r.stderr and "timed out" in r.stderr, r.stderr[-3000:]
+    assert "using step structure 'torch' instead of 'xgmi'" in r.stderr, r.stderr[-3000:]
+    # (each rank prints its own epoch lines, in either order)
+    ep = lambda out: sorted(l for l in out if l.startswith("Epoch:"))
+    assert len(ep(ref)) == 4 and ep(r.stdout.splitlines()) == ep(ref)

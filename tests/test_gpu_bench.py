@@ -51,8 +51,8 @@ def test_bench_transport_calibration(gpu):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     cal = d["config"]["transport_calibration_ms_per_step"]
-    # ('zero', the sharded fc1 update, is a candidate only when PDM_RCCL_MODE forces it)
-    assert set(cal) == {"xgmi", "rccl", "rccl-nocarry", "rccl-side", "rccl-early"}, cal
+    # at most four structures per batch ('zero' and 'side' only when PDM_RCCL_MODE forces them)
+    assert set(cal) == {"xgmi", "xgmi-noxchg", "rccl-nocarry", "rccl"}, cal
     assert d["comm"].get("fallback", []) == []
     assert d["config"]["grad_transport"] == min(cal, key=cal.get)
     # what the data plane saw: a 1-rank RCCL communicator, no xGMI peer to map
@@ -118,11 +118,11 @@ def test_bench_self_spawn_rehearsal(gpu):
 
 def test_bench_calibration_survives_failing_candidates(gpu):
     """Calibration on the real step with injected faults (an exception while the xgmi step
-    is captured, one during rccl-early's timed steps, one in rccl-side's check): those
-    candidates are dropped and recorded, the replicas restored from rank 0 (1-rank RCCL
-    broadcast, bf16 copies re-derived), and the fastest survivor timed."""
+    is captured, one in xgmi-noxchg's check): those candidates are dropped and recorded, the
+    replicas restored from rank 0 (1-rank RCCL broadcast, bf16 copies re-derived), and the
+    fastest survivor timed."""
     env = dict(os.environ, PDM_FORCE_COMM="1",
-               PDM_CALIB_FAULT="0:xgmi:setup,0:rccl-early:timed,0:rccl-side:check")
+               PDM_CALIB_FAULT="0:xgmi:setup,0:xgmi-noxchg:check")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20",
                         "--warmup", "3", "--scaling", "weak"], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=600)
@@ -132,8 +132,60 @@ def test_bench_calibration_survives_failing_candidates(gpu):
     assert set(cal) == {"rccl", "rccl-nocarry"}, cal
     assert d["config"]["grad_transport"] in cal
     notes = " | ".join(d["comm"]["fallback"])
-    for name in ("xgmi", "rccl-early", "rccl-side"):
+    for name in ("xgmi", "xgmi-noxchg"):
         assert f"{name} failed calibration" in notes, notes
+    assert d["value"] > 0
+
+
+def test_bench_calibration_survives_rccl_abort(gpu):
+    """A device stall past a candidate's host deadline on the RCCL data plane (a bounded spin
+    kernel queued behind rccl's steps): the deadline aborts the RCCL communicator, the
+    candidate is dropped, every rank drains its device and joins a fresh communicator
+    (RcclComm.revive), the RCCL reducer is rebuilt on it, and calibration and the timed run
+    continue over the new one."""
+    env = dict(os.environ, PDM_FORCE_COMM="1", PDM_XGMI_TIMEOUT="2", PDM_CALIB_TIMEOUT_S="2",
+               PDM_CALIB_FAULT="0:rccl:spin")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20",
+                        "--warmup", "3", "--scaling", "weak"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    cal = d["config"]["transport_calibration_ms_per_step"]
+    assert set(cal) == {"xgmi", "xgmi-noxchg", "rccl-nocarry"}, cal
+    notes = " | ".join(d["comm"]["fallback"])
+    assert "rccl failed calibration" in notes and "did not finish within" in notes, notes
+    assert "re-created after an abort" in r.stderr
+    assert d["comm"]["rccl_comm_count"] == 1        # the revived communicator answers
+    assert d["value"] > 0
+
+
+def test_bench_calibration_survives_xgmi_device_hang(gpu):
+    """A real device hang in one candidate on one rank: in the two-rank rehearsal (ranks
+    sharing the GPU, gloo data plane, xgmi calibrated against it) rank 1 never launches its
+    persistent xGMI collective, so rank 0's collective waits for rank 1's buckets and rank 1's
+    optimizer for its reduced buckets.  Those device waits give up at PDM_XGMI_TIMEOUT (error
+    words, fail-fast), before the host deadline (timeout + PDM_CALIB_TIMEOUT_S), so nothing
+    is aborted: the candidate is dropped on both ranks from its error word, the replicas are
+    restored from rank 0, the run goes on with the gloo reducer and ends with one JSON line
+    naming xgmi in comm.fallback and bit-equal replicas (bench.py checks the fingerprints)."""
+    from conftest import free_port
+    env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_BENCH_BACKEND="gloo",
+               PDM_XGMI_TIMEOUT="3", PDM_CALIB_TIMEOUT_S="20",
+               PDM_CALIB_FAULT="1:xgmi:devhang")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--steps", "10", "--warmup", "2", "--scaling", "weak"], cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    notes = " | ".join(d["comm"]["fallback"])
+    assert "xgmi failed calibration" in notes and "timed out" in notes, notes
+    assert "did not finish within" not in notes            # no host deadline fired
+    assert d["config"]["grad_transport"] == "torch"
+    assert list(d["config"]["transport_calibration_ms_per_step"]) == ["torch"]
     assert d["value"] > 0
 
 

@@ -6,15 +6,14 @@ from pytorch_distributed_mnist_amd.runtime.structure import StepStructure
 
 def test_defaults_are_production(monkeypatch):
     for k in ("PDM_RCCL_MODE", "PDM_SPLITK_CAP", "PDM_FUSE_FC1", "PDM_BANDS", "PDM_F32_CONV",
-              "PDM_FC1_CARRY_FWD", "PDM_FUSE_HEAD", "PDM_FC1_CARRY_LOCAL"):
+              "PDM_FC1_CARRY_FWD", "PDM_FC1_CARRY_LOCAL"):
         monkeypatch.delenv(k, raising=False)
     s = StepStructure.from_env()
     assert s == StepStructure()
-    assert s.rccl_mode == "carry" and s.splitk_cap == 32 and s.fuse_fc1 and s.bands is None
-    # the fc1 update carried into the next forward (world size > 1): on; fc1_fwd + head in
-    # one launch: off (measured slower, profiles/r5/fc1_head/); carried at world size 1 too
-    # where that is faster (profiles/r5/fc1_carry_local/)
-    assert s.fc1_carry_fwd and not s.fuse_head and s.fc1_carry_local
+    assert s.rccl_mode == "nocarry" and s.splitk_cap == 32 and s.fuse_fc1 and s.bands is None
+    # the fc1 update carried into the next forward (world size > 1): on; carried at world
+    # size 1 too where that is faster (profiles/r5/fc1_carry_local/)
+    assert s.fc1_carry_fwd and s.fc1_carry_local
 
 
 def test_from_env_reads_each_knob(monkeypatch):
@@ -25,12 +24,11 @@ def test_from_env_reads_each_knob(monkeypatch):
     monkeypatch.setenv("PDM_F32_CONV", "exact")
     monkeypatch.setenv("PDM_KEEP_GRADS", "1")
     monkeypatch.setenv("PDM_FC1_CARRY_FWD", "0")
-    monkeypatch.setenv("PDM_FUSE_HEAD", "1")
     monkeypatch.setenv("PDM_FC1_CARRY_LOCAL", "0")
     s = StepStructure.from_env()
     assert (s.rccl_mode, s.splitk_cap, s.fuse_fc1, s.bands, s.f32_conv, s.keep_grads) == \
         ("early", 16, False, 3, "exact", True)
-    assert (s.fc1_carry_fwd, s.fuse_head, s.fc1_carry_local) == (False, True, False)
+    assert (s.fc1_carry_fwd, s.fc1_carry_local) == (False, False)
     assert s.with_(rccl_mode="nocarry").rccl_mode == "nocarry"
 
 
