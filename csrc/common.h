@@ -123,22 +123,7 @@ __device__ __forceinline__ float4 pdm_slab_load4(const float4* p) { return *p; }
 // Bookkeeping done by exactly one thread of a kernel that no other kernel of the
 // same step reads concurrently (see runtime/gpu_step.py: the "middle" kernel
 // advances the data-step and optimizer-step counters).
-// Debug build only (PDM_DEBUG_BOUNDS=1 python -m pytorch_distributed_mnist_amd.build):
-// device-side index checks that print the failing site and trap; compiled out otherwise.
-#ifdef PDM_DEBUG_BOUNDS
-#define PDM_CHECK(cond, what, v0, v1)                                                      \
-  do {                                                                                     \
-    if (!(cond)) {                                                                         \
-      printf("PDM_CHECK failed: %s (%lld, %lld) block %d thread %d\n", what, (long long)(v0), \
-             (long long)(v1), (int)blockIdx.x, (int)threadIdx.x);                           \
-      __builtin_trap();                                                                    \
-    }                                                                                      \
-  } while (0)
-#else
-#define PDM_CHECK(cond, what, v0, v1) \
-  do {                                \
-  } while (0)
-#endif
+#include "pdm_check.h"
 
 // One 256-thread workgroup: metrics[0] += sum_j slab[j][col], metrics[1] += sum_j
 // slab[j][col + 1] over the nslab per-workgroup slabs (row stride `stride` floats): the

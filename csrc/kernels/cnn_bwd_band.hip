@@ -175,6 +175,11 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
   const int pr0 = band == 0 ? 0 : d0 / 2 - 1;    // first staged pooled row
   const int npr = d0 / 2 + R / 2 - pr0;          // staged pooled rows
   const int pown0 = d0 / 2;                      // first own pooled row
+  // band geometry: the staged pooled rows fit the scatter's items, and the band's a1 / x rows
+  // (incl. halos and the last band's two extra a1 rows) stay inside the image
+  PDM_CHECK(npr >= 1 && npr <= L::PR, "cnn_bwd_band staged pooled rows", npr, L::PR);
+  PDM_CHECK(d0 + L::AR <= H1 && d0 + L::XR <= IMG, "cnn_bwd_band a1 / x rows past the image",
+            d0, band);
   bf16* xs = reinterpret_cast<bf16*>(smem + L::XS);
   float* out = slab + (int64_t)blockIdx.x * CNN_CONV_SLAB;
   PDM_STAMP(0);
@@ -225,6 +230,7 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
   {
     const int zlo = 2 * pr0 - (d0 - 2);          // first scattered local row (0 or 2)
     const int zhi = zlo + 2 * npr;               // = R + 2
+    PDM_CHECK(zlo >= 0 && zhi <= L::ZR, "cnn_bwd_band scattered dz2 rows", zlo, zhi);
     constexpr int NZ = 4 + L::ZR * DSB;          // candidate pixels: zero block + all rows
     for (int i = tid; i < NZ * 8; i += BTH) {
       const int pix = i >> 3, ch = i & 7;
@@ -253,6 +259,8 @@ __global__ __launch_bounds__(BTH, 1) void cnn_bwd_band_kernel(
       const int pyl = pl / HP, px = pl - pyl * HP;
       const int py = pr0 + pyl;
       const int lr = 2 * py - (d0 - 2);          // local dz2 row of the window's top row
+      // the window's two rows inside the staged halo image [d0 - 2, d0 + R + 3)
+      PDM_CHECK(lr >= 0 && lr + 1 < L::ZR, "cnn_bwd_band halo dz2 row", lr, L::ZR);
       const int base = L::DZ + (lr * DSB + 2 * px) * 128;
       const int b0 = 2 * px + ch;                // + 4 (lr + dy) + dx; 4 lr = 0 mod 8
       const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};

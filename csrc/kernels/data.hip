@@ -24,8 +24,9 @@ __global__ __launch_bounds__(256) void gather_epoch_kernel(const uint8_t* __rest
   if (blockIdx.x == 0 && threadIdx.x == 0 && step != nullptr) *step = step_value;
   // 16 rows per workgroup pass; a grid smaller than the row count strides over the rest
   for (int row = blockIdx.x * 16 + (threadIdx.x >> 4); row < n; row += gridDim.x * 16) {
-    const int src = idx[row];
-    PDM_CHECK(src >= 0 && src < nimg, "gather_epoch index", src, nimg);
+    const int src_u = idx[row];
+    PDM_CHECK(src_u >= 0 && src_u < nimg, "gather_epoch index", src_u, nimg);
+    const int src = min(max(src_u, 0), nimg - 1);   // (a bad host index reads a valid row)
     const uint4* s = reinterpret_cast<const uint4*>(images + (int64_t)src * 784);
     uint4* d = reinterpret_cast<uint4*>(out_images + (int64_t)row * 784);
     for (int c = threadIdx.x & 15; c < 49; c += 16) d[c] = s[c];

@@ -62,6 +62,8 @@ __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg
     const int tr0 = (lb / tiles_c) * FCC_TR, tc0 = (lb % tiles_c) * FCC_TC;
     if (lb < FCC_TILES) {
       const int row = tr0 + r, col0 = tc0 + c8;
+      PDM_CHECK(row < HID && col0 + 8 <= FEAT, "fc_carry tile position", row, col0);
+      PDM_CHECK(fcc_tpos(c8 + 7, r) < FCC_TC * FCC_TR, "fc_carry LDS transpose slot", c8, r);
       const int64_t e = (int64_t)row * FEAT + col0;
       float pv[8], gv[8], mv[8];
 #pragma unroll
@@ -97,6 +99,8 @@ __device__ __forceinline__ void fc_carry_role(const FcUpdate& u, int wg, int nwg
     if (lb < FCC_TILES) {
       // transposed store: thread -> (col c, 8 consecutive rows) = one 16-B store
       const int c = t >> 2, rr = (t & 3) * 8;
+      PDM_CHECK(tr0 + rr + 8 <= HID && tc0 + c < FEAT, "fc_carry transposed tile", tr0 + rr,
+                tc0 + c);
       *reinterpret_cast<bf16x8*>(u.shadow_t_next + shadow_t_pos(1, HID, tr0 + rr, tc0 + c)) =
           *reinterpret_cast<const bf16x8*>(&tile[fcc_tpos(c, rr)]);
     }

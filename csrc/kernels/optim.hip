@@ -51,6 +51,11 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
   }
   const OptSeg s = a.seg[si];
   const int lb = blockIdx.x - s.first_block;
+  // segment table: this workgroup lies inside its segment's block range
+  PDM_CHECK(si < nseg && lb >= 0 &&
+                (int)blockIdx.x < (si + 1 < nseg ? fb[si + 1]
+                                                 : (int)gridDim.x - (metrics != nullptr ? 1 : 0)),
+            "optim segment table", si, lb);
   if (bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
   if (xgp != nullptr) {
     // xgmi streamed mode: publish the last bucket (every workgroup stores the same value,
@@ -117,6 +122,7 @@ __global__ __launch_bounds__(256) void optim_kernel(OptArgs a) {
     const int e0 = lb * 64;
     // clamped to the segment's last float4 group (the slab row holds the whole group)
     const int col = s.slab_col0 + min(e0 + 4 * c4, (((int)numel + 3) & ~3) - 4);
+    PDM_CHECK(col >= 0 && col + 4 <= s.slab_stride, "optim slab column", col, s.slab_stride);
     const float4* sp = reinterpret_cast<const float4*>(s.slab + col);
     const int64_t st4 = s.slab_stride / 4;
     // the update's operands are loaded ahead of the slab reduction (one memory round trip

@@ -115,6 +115,9 @@ __device__ __forceinline__ bool xg_channel(const XgmiArgs& a, int w, int W, unsi
   const int lo = w * per;
   const int par = two ? 0 : (int)(gen & 1u);            // one-shot stage double buffer
   const int row4 = c4;                                  // stage row length (float4)
+  // flag slot of this workgroup; the two-shot chunks (one per rank) cover the bucket
+  PDM_CHECK(w >= 0 && w < W && W <= XG_MAX_WG, "xgmi channel flag slot", w, W);
+  PDM_CHECK(!two || (long long)c4 * 4 * N >= a.n, "xgmi two-shot chunks", c4, a.n);
 
   // phase 0: push slice w of chunk d (two-shot) / of the bucket (one-shot) into row r
   // of rank d's stage.  Workgroups start at different peers so all N-1 links carry

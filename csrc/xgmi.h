@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pdm_check.h"
+
 constexpr int XG_MAX_RANKS = 8;
 constexpr int XG_MAX_WG = 128;     // workgroups per collective launch
 constexpr int XG_MAX_CH = 4;       // channels (one per gradient bucket)
@@ -190,6 +192,9 @@ __device__ __forceinline__ bool xg_wait_done(unsigned* loc, int ch, unsigned mul
 __device__ __forceinline__ bool xg_exchange(const XgmiExch& x, int slot, long long bl, bool valid,
                                             float& v, int* s_ok) {
   const int N = x.nranks, r = x.rank, tid = threadIdx.x;
+  // one flag slot per slab workgroup; the element inside the bucket's stage row
+  PDM_CHECK(slot >= 0 && slot < XG_XSLOTS, "xgmi exchange flag slot", slot, XG_XSLOTS);
+  PDM_CHECK(!valid || (bl >= 0 && bl < x.n), "xgmi exchange stage offset", bl, x.n);
   if (N == 1) return true;
   const unsigned gen = __hip_atomic_load(x.gen + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const long long par = gen & 1u;
