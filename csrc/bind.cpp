@@ -868,6 +868,11 @@ at::Tensor read_stamps(const std::string& which) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) kernels + RCCL runtime for pytorch_distributed_mnist_amd";
+#ifdef PDM_DEBUG_BOUNDS
+  m.attr("DEBUG_BOUNDS") = true;     // PDM_CHECK sites compiled in (tools/gpu_r6_debug.sh)
+#else
+  m.attr("DEBUG_BOUNDS") = false;
+#endif
   m.attr("LIN_ROWS") = LIN_ROWS;
   m.attr("LIN_SLAB") = LIN_SLAB;
   m.attr("OPT_ADAM") = OPT_ADAM;

@@ -369,3 +369,27 @@ def test_epoch_gather_ahead_bit_identical(gpu, model, dtype, opt):
     assert torch.equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1]
 
+
+
+def test_debug_bounds_checks_report(gpu, capfd):
+    """The debug-bounds build (PDM_DEBUG_BOUNDS=1, tools/gpu_r6_debug.sh) reports a violated
+    check from the device without trapping: a sampler index past the dataset makes
+    gather_epoch print its PDM_CHECK line, clamps the row and goes on.  (Skipped on the
+    production build, where the checks are compiled out.)"""
+    from pytorch_distributed_mnist_amd.ops import _ext
+    C = _ext.require()
+    if not C.DEBUG_BOUNDS:
+        pytest.skip("production build: PDM_CHECK sites compiled out")
+    n = 64
+    images = torch.randint(0, 255, (n, 784), dtype=torch.uint8, device="cuda")
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device="cuda")
+    idx = torch.arange(16, dtype=torch.int32, device="cuda")
+    idx[3] = n + 5                                    # past the dataset
+    out_i = torch.empty(16, 784, dtype=torch.uint8, device="cuda")
+    out_l = torch.empty(16, dtype=torch.int32, device="cuda")
+    C.gather_epoch(images, labels, idx, out_i, out_l, None, None, 0, 0)
+    torch.cuda.synchronize()
+    out = capfd.readouterr().out
+    assert "PDM_CHECK failed: gather_epoch index" in out, out
+    assert torch.equal(out_i[3], images[n - 1])      # clamped to the last row
+    assert torch.equal(out_i[4], images[4])
