@@ -62,6 +62,7 @@ def compile_flags(abi: int, inc):
              "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
              f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
              "-Wno-unused-result", "-Wno-deprecated-declarations",
+             "-Werror=misleading-indentation",
              f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}"]
     flags += [f"-I{p}" for p in inc]
     if knobs.get("PDM_DEBUG_BOUNDS"):
