@@ -10,6 +10,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -119,6 +120,15 @@ __device__ __forceinline__ void st_ho(T* p, T v) {
 // Non-temporal (streaming) forms of both measured slower (round 4, docs/kernels.md).
 __device__ __forceinline__ void pdm_slab_store(float* p, float v) { st_ho<1>(p, v); }
 __device__ __forceinline__ float4 pdm_slab_load4(const float4* p) { return *p; }
+// 16 B of a slab, floats [e, e + 4) of the (workgroup-uniform) slab `base`, e % 4 == 0, in
+// one write-through store (sc1, like st_ho<1>): a quarter of the store instructions of four
+// pdm_slab_store calls, which a slab tail can be issue-bound on.  A buffer store, not inline
+// asm: the compiler must see the store to keep its data registers from being overwritten
+// while it is in flight (an asm global_store_dwordx4 measured non-deterministic slabs).
+__device__ __forceinline__ void pdm_slab_store4(float* base, int e, f32x4 v) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, e * 4, 0, 16 /* sc1 */);
+}
 
 // Bookkeeping done by exactly one thread of a kernel that no other kernel of the
 // same step reads concurrently (see runtime/gpu_step.py: the "middle" kernel

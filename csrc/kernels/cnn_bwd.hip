@@ -436,20 +436,22 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
   // ---- 1. loads
   uint32_t xw = 0;
   if (tid < 196) xw = reinterpret_cast<const uint32_t*>(xg + (int64_t)img * 784)[tid];
-  float w1v[2][4];
+  // conv1 weights and bias: one 16-B load per (mt) each -- lane group g's taps 4g .. 4g + 3
+  // of channel 16mt + i16 are 4 consecutive floats (g = 2: tap 8 is the last of taps 5 .. 8;
+  // g = 3 has no taps).  (16 dword loads per lane before: every CU of an XCD fetching the
+  // same 1.2 KB delayed the dpool / pmask loads behind them by ~2k cycles, stamps.)
   int toff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int tap = 4 * g + j;
     toff[j] = (tap < 9) ? (tap / 3) * IMG + (tap % 3) : IMG * IMG;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) w1v[mt][j] = w1[(mt * 16 + i16) * 9 + min(tap, 8)];
   }
-  f32x4 b1v[2];
+  f32x4 w1q[2], b1v[2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) b1v[mt][r] = b1[mt * 16 + 4 * g + r];
+  for (int mt = 0; mt < 2; ++mt) {
+    __builtin_memcpy(&w1q[mt], w1 + (mt * 16 + i16) * 9 + min(4 * g, 5), 16);   // 4-B aligned
+    __builtin_memcpy(&b1v[mt], b1 + mt * 16 + 4 * g, 16);
+  }
   const uint4* dpv = reinterpret_cast<const uint4*>(dpool + (int64_t)img * FEAT);
   const uint2* mkv = reinterpret_cast<const uint2*>(pmask + (int64_t)img * FEAT);
   uint4 d[3];
@@ -504,7 +506,8 @@ __device__ __forceinline__ void bwd_load_image(char* smem, int img, const uint8_
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w1f[mt][j] = to_bf16(4 * g + j < 9 ? w1v[mt][j] : 0.f);
+    for (int j = 0; j < 4; ++j)
+      w1f[mt][j] = to_bf16(4 * g + j < 9 ? (g == 2 ? w1q[mt][3] : w1q[mt][j]) : 0.f);
   __syncthreads();
   if (threadIdx.x == 0) PDM_STAMP_VAL(13, PDM_CLOCK());
   // conv1 recompute: D[co][pixel] on mfma_f32_16x16x16_bf16 (same math as cnn_fwd), over
@@ -830,13 +833,16 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)   // waves 2,3: pair 4 is a discarded duplicate
-            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ac[mt], Bc[pi], acc[pi][mt], 0, 0, 0);
+            acc[pi][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bc[pi], Ac[mt], acc[pi][mt], 0, 0, 0);
         }
       });
     };
     // the accumulators persist across the workgroup's images; after the last image they
-    // are stored while the dgrad waves are still computing.  dW2[co][tap][ci]: rows
-    // co = 16mt + 4g + r, col ci = 16nt + i16
+    // are stored while the dgrad waves are still computing.  The MFMAs compute dW2^T (B and
+    // A operands swapped: the same products, summed in the same order), so lane (g, i16)
+    // holds co = 16mt + i16, ci = 16nt + 4g + r: 4 consecutive floats of dW2[co][tap][ci],
+    // one 16-B store per (pair, co tile) -- 20 instead of 80 store instructions per wave
+    // (the tail was store-issue-bound: 4.3k cycles, stamps)
     auto per_image = [&](auto first, auto one, int i, bool last) __attribute__((always_inline)) {
       const int img = blockIdx.x * ipb + i;
       if (img < B) bwd_load_image<decltype(first)::value>(smem, img, xg, dpool, pmask, w1, b1, w2t, db2p);
@@ -858,12 +864,10 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void cnn_bwd_kernel(
           const int pair = wave + 4 * pi;
           const int tap = pair >> 1, nt = pair & 1;
           int o;   // laundered: 20 hoisted 64-bit store addresses would be spilled
-          asm volatile("v_mov_b32 %0, %1" : "=v"(o) : "v"(4 * g * 288 + i16));
+          asm volatile("v_mov_b32 %0, %1" : "=v"(o) : "v"(i16 * 288 + 4 * g));
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              pdm_slab_store(&out[o + (mt * 16 + r) * 288 + tap * 32 + nt * 16], acc[pi][mt][r]);
+            pdm_slab_store4(out, o + mt * 16 * 288 + tap * 32 + nt * 16, acc[pi][mt]);
         }
         PDM_STAMP(3);
       }
