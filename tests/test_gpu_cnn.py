@@ -371,6 +371,32 @@ def test_epoch_gather_ahead_bit_identical(gpu, model, dtype, opt):
 
 
 
+@pytest.mark.parametrize("n,max_wgs,host", [(1, 0, False), (63, 0, False), (64, 0, True),
+                                            (1000 + 37, 0, True), (5000, 7, False)])
+def test_gather_epoch_matches_indexing(gpu, n, max_wgs, host):
+    """The epoch gather (data.hip: 64 rows per workgroup pass, the pass's indices read once,
+    from device memory or -- the training path -- a pinned host buffer) equals plain
+    indexing for images and labels, for row counts off the pass size and for a capped grid
+    that strides over the rows; the step counters are reset."""
+    from pytorch_distributed_mnist_amd.ops import _ext
+    C = _ext.require()
+    nimg = 3000
+    g = torch.Generator().manual_seed(n)
+    images = torch.randint(0, 256, (nimg, 784), dtype=torch.uint8, generator=g).cuda()
+    labels = torch.randint(0, 10, (nimg,), dtype=torch.int32, generator=g).cuda()
+    idx = torch.randint(0, nimg, (n,), dtype=torch.int32, generator=g)
+    idx = idx.pin_memory() if host else idx.cuda()
+    out_i = torch.full((n + 3, 784), 7, dtype=torch.uint8, device="cuda")
+    out_l = torch.full((n + 3,), -1, dtype=torch.int32, device="cuda")
+    ctr = torch.full((4,), 9, dtype=torch.int64, device="cuda")
+    C.gather_epoch(images, labels, idx, out_i, out_l, ctr, None, 0, max_wgs)
+    torch.cuda.synchronize()
+    il = idx.long().cuda()
+    assert torch.equal(out_i[:n], images[il]) and torch.equal(out_l[:n], labels[il])
+    assert bool((out_i[n:] == 7).all()) and bool((out_l[n:] == -1).all())   # nothing past n
+    assert int(ctr.abs().sum()) == 0
+
+
 def test_debug_bounds_checks_report(gpu, capfd):
     """The debug-bounds build (PDM_DEBUG_BOUNDS=1, tools/gpu_r6_debug.sh) reports a violated
     check from the device without trapping: a sampler index past the dataset makes
