@@ -382,7 +382,12 @@ def main():
 
         def mark(what):
             if dbg:
-                marks.append((what, time.perf_counter()))
+                ev = None
+                if dbg == "events" and torch.cuda.is_available():
+                    # PDM_BENCH_DEBUG=events: also where the device stream is at each mark
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                marks.append((what, time.perf_counter(), ev))
 
         def next_epoch():
             mark("get")
@@ -424,14 +429,20 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             marks.clear()
+            mark("start")
             imgs = run(k)
             mark("sync")
             sync("timed steps")
             mark("end")
             if dbg and rank == 0:
                 print("bench.py: window " + " | ".join(f"{w} @{1e6 * (t - t0):.0f}"
-                                                       for w, t in marks), file=sys.stderr,
+                                                       for w, t, _ in marks), file=sys.stderr,
                       flush=True)
+                evs = [(w, e) for w, _, e in marks if e is not None]
+                if evs:
+                    print("bench.py: window on the device " + " | ".join(
+                        f"{w} @{1e3 * evs[0][1].elapsed_time(e):.1f}" for w, e in evs),
+                        file=sys.stderr, flush=True)
             barrier()
             torch.cuda.synchronize()
             return allmax(time.perf_counter() - t0), imgs

@@ -59,7 +59,8 @@ KNOBS: Dict[str, tuple] = {
                        "chain (fc1 update sharded over 128 / N rows, collectives stubbed)"),
     "PDM_BENCH_BACKEND": ("nccl", "rehearsal", "gloo: multi-rank bench on one GPU"),
     "PDM_BENCH_BOUNDARY": ("1", "diag", "0: no epoch boundary inside the timed window"),
-    "PDM_BENCH_DEBUG": (None, "diag", "1: print the host timeline of the timed window"),
+    "PDM_BENCH_DEBUG": (None, "diag", "1: print the host timeline of the timed window; "
+                        "events: the device timeline too (CUDA events at the marks)"),
     "PDM_BENCH_FAIL_RANK": (None, "diag", "fault injection: this rank exits (dry runs)"),
     "PDM_BENCH_SPAWNED": (None, "internal", "set by bench.py on the ranks it starts"),
     "PDM_CALIB_FAULT": (None, "diag", "fault injection into calibration: "

@@ -270,6 +270,24 @@ class GpuStepBase:
             return [(False, False)] * nreplays
         return [(i > 0, i < nreplays - 1) for i in range(nreplays)]
 
+    def _plan(self, B: int, n: int):
+        """The replays of ``train_steps(B, n)``: [(steps, carry in, carry out)] -- n // GRAPH_STEPS
+        full graphs, then one graph per set bit of the remainder, largest first."""
+        k = self.GRAPH_STEPS
+        r = n % k
+        sizes = [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]
+        return [(s, ci, co) for s, (ci, co) in zip(sizes, self._carry_flags(B, len(sizes)))]
+
+    def _variants(self, B: int, sizes):
+        """Every (steps, phase, carry in, carry out) graph some ``_plan(B, n)`` replays, for the
+        given graph sizes.  A graph smaller than GRAPH_STEPS only stands for a set bit of the
+        remainder and those come in descending order, so the 1-step graph is always a call's
+        last replay and never carries out."""
+        flags = ((False, False), (False, True), (True, True), (True, False)) \
+            if self.carries_across_graphs(B) else ((False, False),)
+        return [(n, ph, ci, co) for n in sizes for ph in range(self.phase_period)
+                for ci, co in flags if not (co and n == 1 and self.GRAPH_STEPS > 1)]
+
     def prepare(self, B: int, sizes=None) -> None:
         """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, or
         `sizes`, in every step phase), so no capture or first-launch upload lands inside a
@@ -277,10 +295,7 @@ class GpuStepBase:
         when replayed."""
         if not self.use_graphs:
             return
-        flags = ((False, False), (False, True), (True, True), (True, False)) \
-            if self.carries_across_graphs(B) else ((False, False),)
-        for n, ph, (ci, co) in ((n, ph, f) for n in (sizes or self.GRAPH_SIZES)
-                                for ph in range(self.phase_period) for f in flags):
+        for n, ph, ci, co in self._variants(B, sizes or self.GRAPH_SIZES):
             g = self._graph(B, n, ph, ci, co)
             try:
                 exe = g.raw_cuda_graph_exec()
@@ -296,10 +311,7 @@ class GpuStepBase:
         if n <= 0:
             return
         if self.use_graphs:
-            k = self.GRAPH_STEPS
-            r = n % k
-            sizes = [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]
-            flags = self._carry_flags(B, len(sizes))
+            plan = self._plan(B, n)
             if self.collective_outside():
                 # one persistent collective for all n steps, launched eagerly on its own
                 # stream beside the graph replays: the steps hand it their buckets through
@@ -309,11 +321,11 @@ class GpuStepBase:
                 # capture synchronizes the device, which would wait for a running
                 # collective that waits for steps not yet launched.
                 ph = self.phase
-                for size, (ci, co) in zip(sizes, flags):
+                for size, ci, co in plan:
                     self._graph(B, size, ph, ci, co)
                     ph = (ph + size) % self.phase_period
                 self.reducer.begin(n, self.collective_channels(), self.collective_wide(B))
-            for size, (ci, co) in zip(sizes, flags):
+            for size, ci, co in plan:
                 self._issue_ahead()
                 self._replay(B, size, ci, co)
                 self._ctr_host += size

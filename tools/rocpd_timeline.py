@@ -21,11 +21,16 @@ def main():
     ap.add_argument("--skip", type=int, default=100)
     ap.add_argument("--count", type=int, default=40)
     ap.add_argument("--title", default="kernel timeline")
+    ap.add_argument("--last", type=int, default=None,
+                    help="start N dispatches before the end of the trace (the timed window of a "
+                         "short bench.py run sits near the end)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = [(short(n), s, e) for n, s, e in
             c.execute("select name, start, end from kernels order by start").fetchall()]
-    if a.after:
+    if a.last:
+        i0 = max(0, len(rows) - a.last)
+    elif a.after:
         hits = [i for i, r in enumerate(rows) if r[0].startswith(a.after)]
         i0 = hits[min(a.skip, len(hits) - 1)] if hits else 0
     else:
