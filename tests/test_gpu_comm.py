@@ -199,6 +199,56 @@ def test_fc1_grad_arena_is_current_with_carried_updates(gpu, monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize("B", [32, 256])
+def test_calibration_candidates_as_composed_match_local(gpu, B):
+    """Every step structure bench.py's N > 1 calibration can pick (bench.step_candidates), with
+    the production defaults composed as a real job runs them -- the xgmi streamed step with the
+    in-launch conv exchange, the persistent collective outside the graphs, the fc1 update
+    carried into the next forward and across graph replays; xgmi without the exchange; RCCL
+    nocarry with the carried update; RCCL carry (B >= 256) / early (B < 256) -- through a
+    forced 1-rank communicator, over two epochs of graph replays with the ragged tail, gives
+    the world-size-1 path's weights, momentum and bf16 W1 / W1^T bit for bit.  (Each change is
+    also pinned against its neighbour above; this pins the combinations.)"""
+    from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
+    from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
+    from pytorch_distributed_mnist_amd.runtime.program import build_local_program
+    train = synthetic_split(B * 19 + 40, True)
+    test = synthetic_split(256, False)
+    cands = [("local", None, None, None), ("xgmi", "xgmi", "carry", True),
+             ("xgmi-noxchg", "xgmi", "carry", False), ("rccl-nocarry", "rccl", "nocarry", True),
+             ("rccl" if B >= 256 else "rccl-early", "rccl", "carry" if B >= 256 else "early",
+              True)]
+    out = {}
+    for name, transport, mode, xchg in cands:
+        comm = _comm(gpu) if transport else None
+        p = build_local_program("cnn", "bf16", "cuda", B, train, test, optimizer="sgd", lr=0.05,
+                                momentum=0.9, seed=4, use_graphs=True, comm=comm,
+                                force_comm=comm is not None, transport=transport or "rccl")
+        if transport:
+            assert p.reducer.kind == transport
+            p.gpu.set_rccl_mode(mode, invalidate=False)
+            p.gpu.xgmi_exchange = xchg and p.structure.xgmi_exchange
+            p.gpu.invalidate_graphs()
+            if transport == "xgmi":
+                assert p.gpu._xchg() == xchg
+        p.optimizer.sync_hyperparams()
+        for epoch in range(2):
+            p.set_train_indices(distributed_indices(len(train), 1, 0, epoch))
+            p.train_epoch()
+        torch.cuda.synchronize()
+        p.reducer.check()
+        p.gpu.check_device()
+        o = p.optimizer
+        out[name] = (p.arena.params.clone(), o.momentum_buffer.clone(), p.gpu.wf1.clone(),
+                     p.gpu.current_wf1t().clone())
+        if transport:
+            p.reducer.close()
+            comm.close()
+    for name, got in out.items():
+        for a, b in zip(out["local"], got):
+            assert torch.equal(a, b), name
+
+
 def test_rccl_comm_count(gpu):
     comm = _comm(gpu)
     assert comm.comm_count() == 1
