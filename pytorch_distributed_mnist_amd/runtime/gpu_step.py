@@ -127,7 +127,7 @@ class GpuStepBase:
             self.C.gather_epoch(self.train_images, self.train_labels, buf[0],
                                 self.ep_images.view(-1, 784)[half * n:(half + 1) * n],
                                 self.ep_labels[half * n:(half + 1) * n],
-                                # one workgroup per 16 rows (grid-striding ones taking
+                                # one workgroup per 64 rows (grid-striding ones taking
                                 # fewer CUs beside the steps measured no better)
                                 max_wgs=0)
             ev = torch.cuda.Event()
