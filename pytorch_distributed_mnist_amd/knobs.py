@@ -36,7 +36,7 @@ KNOBS: Dict[str, tuple] = {
                             "fc1_bwd at every batch instead of carrying it into the next "
                             "forward launch where that is faster (B > 128)"),
     "PDM_BANDS": (None, "structure", "row bands per image in the conv backward (1 = off)"),
-    "PDM_GRAPH_STEPS": ("8", "structure", "training steps per captured hipGraph (power of two)"),
+    "PDM_GRAPH_STEPS": ("16", "structure", "training steps per full captured hipGraph (a remainder replays one graph of its own size)"),
     "PDM_FUSE_LIN_REDUCE": ("1", "structure", "0: separate lin_reduce at world size 1 (Linear)"),
     "PDM_F32_CONV": ("x3", "structure", "fp32 CNN conv2 products: x3 (split-bf16) / exact"),
     "PDM_F32_IPB": (None, "structure", "images per fp32 (exact) conv-backward workgroup"),

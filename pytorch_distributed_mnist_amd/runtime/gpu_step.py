@@ -26,11 +26,9 @@ from ..ops import _ext
 from .. import knobs
 
 
-_GRAPH_STEPS = int(knobs.get("PDM_GRAPH_STEPS", "8"))   # steps per graph: a power of two
-if _GRAPH_STEPS <= 0 or _GRAPH_STEPS & (_GRAPH_STEPS - 1):
-    # train_steps splits a remainder into the set bits of GRAPH_SIZES: other sizes would
-    # replay the wrong number of steps and desynchronise the device and host counters
-    raise ValueError(f"PDM_GRAPH_STEPS must be a power of two, got {_GRAPH_STEPS}")
+_GRAPH_STEPS = int(knobs.get("PDM_GRAPH_STEPS", "16"))  # steps per full graph
+if _GRAPH_STEPS <= 0:
+    raise ValueError(f"PDM_GRAPH_STEPS must be positive, got {_GRAPH_STEPS}")
 
 
 def make_gpu_step(prog, use_graphs: bool = True):
@@ -223,9 +221,9 @@ class GpuStepBase:
     # list, graph-replay-floor) — more than a whole small step's GPU time — so
     # steps are captured GRAPH_STEPS at a time (identical steps: the batch comes
     # from the device counter) and a run of n steps replays n // GRAPH_STEPS
-    # multi-step graphs plus one graph per set bit of the remainder (4, 2, 1 steps).
+    # multi-step graphs plus one graph of the remainder.
     GRAPH_STEPS = _GRAPH_STEPS
-    GRAPH_SIZES = tuple(_GRAPH_STEPS >> i for i in range(_GRAPH_STEPS.bit_length()))
+    GRAPH_SIZES = tuple(range(_GRAPH_STEPS, 0, -1))
 
     def carries_across_graphs(self, B: int) -> bool:
         """Whether a step of batch B leaves work to the next one (CnnStep: the carried fc1 update), so
@@ -272,21 +270,21 @@ class GpuStepBase:
 
     def _plan(self, B: int, n: int):
         """The replays of ``train_steps(B, n)``: [(steps, carry in, carry out)] -- n // GRAPH_STEPS
-        full graphs, then one graph per set bit of the remainder, largest first."""
+        full graphs, then one graph of the remainder (each graph boundary leaves the queue
+        idle for ≈ 9 us: profiles/r6/window/)."""
         k = self.GRAPH_STEPS
         r = n % k
-        sizes = [k] * (n // k) + [s for s in self.GRAPH_SIZES[1:] if r & s]
+        sizes = [k] * (n // k) + ([r] if r else [])
         return [(s, ci, co) for s, (ci, co) in zip(sizes, self._carry_flags(B, len(sizes)))]
 
     def _variants(self, B: int, sizes):
         """Every (steps, phase, carry in, carry out) graph some ``_plan(B, n)`` replays, for the
-        given graph sizes.  A graph smaller than GRAPH_STEPS only stands for a set bit of the
-        remainder and those come in descending order, so the 1-step graph is always a call's
-        last replay and never carries out."""
+        given graph sizes.  A graph smaller than GRAPH_STEPS only stands for the remainder,
+        which is always a call's last replay, so it never carries out."""
         flags = ((False, False), (False, True), (True, True), (True, False)) \
             if self.carries_across_graphs(B) else ((False, False),)
         return [(n, ph, ci, co) for n in sizes for ph in range(self.phase_period)
-                for ci, co in flags if not (co and n == 1 and self.GRAPH_STEPS > 1)]
+                for ci, co in flags if not (co and n < self.GRAPH_STEPS)]
 
     def prepare(self, B: int, sizes=None) -> None:
         """Capture and upload every graph ``train_steps(B, n)`` replays (GRAPH_SIZES, or

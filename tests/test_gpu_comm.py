@@ -9,6 +9,9 @@ import pytest
 import torch
 
 from conftest import REPO
+from pytorch_distributed_mnist_amd.runtime.gpu_step import GpuStepBase
+
+GRAPH_STEPS = GpuStepBase.GRAPH_STEPS
 
 pytestmark = pytest.mark.gpu
 
@@ -83,7 +86,7 @@ def test_cnn_step_through_rccl_reducer_matches_local(gpu, carry, B):
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.runtime.program import build_local_program
-    train = synthetic_split(B * 9 + 40, True)
+    train = synthetic_split(B * (GRAPH_STEPS + 1) + 40, True)   # a full graph, a 1-step graph
     test = synthetic_split(256, False)
     out = []
     for force in (False, True):
@@ -110,12 +113,12 @@ def test_fc1_update_carried_into_forward_is_bit_identical(gpu, transport, B):
     """World size > 1 (forced 1-rank communicator; RCCL nocarry and the xgmi in-launch-exchange
     step): step k's fc1 update runs in extra workgroups of step k+1's forward launch
     (kernels/fc_carry.h) instead of the optimizer.  Weights, momentum and both bf16 copies of W1
-    must equal the optimizer-run update, over graph-captured 8-step sequences (7 carried
-    updates each), a sequence of one and the ragged tail."""
+    must equal the optimizer-run update, over a graph-captured full sequence (GRAPH_STEPS - 1
+    carried updates), a sequence of one and the ragged tail."""
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.runtime.program import build_local_program
-    train = synthetic_split(B * 9 + 40, True)
+    train = synthetic_split(B * (GRAPH_STEPS + 1) + 40, True)   # a full graph, a 1-step graph
     test = synthetic_split(256, False)
     out = []
     for carry in (False, True):
@@ -148,11 +151,11 @@ def test_fc1_update_carried_at_world_size_1_is_bit_identical(gpu, B, monkeypatch
     """World size 1 with fc1_carry_local: fc1_bwd stores the fc1-weight gradient and the next
     forward launch updates from it, instead of the update fused into fc1_bwd's weight tiles.
     Same update, same bits: weights, momentum, W1 and the W1^T the next fc1_bwd reads, over
-    two epochs of 8-step graphs, a sequence of one and a (banded, fused) ragged tail."""
+    two epochs of full graphs, a sequence of one and a (banded, fused) ragged tail."""
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.runtime.program import build_local_program
-    train = synthetic_split(B * 9 + 40, True)
+    train = synthetic_split(B * (GRAPH_STEPS + 1) + 40, True)   # a full graph, a 1-step graph
     test = synthetic_split(256, False)
     out = []
     for carry in ("0", "1"):
@@ -181,7 +184,7 @@ def test_fc1_grad_arena_is_current_with_carried_updates(gpu, monkeypatch):
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.runtime.program import build_local_program
     B = 256
-    train = synthetic_split(B * 9 + 40, True)
+    train = synthetic_split(B * (GRAPH_STEPS + 1) + 40, True)   # a full graph, a 1-step graph
     test = synthetic_split(256, False)
     out = []
     for keep in ("0", "1"):

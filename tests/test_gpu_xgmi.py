@@ -52,8 +52,9 @@ def test_cnn_step_through_xgmi_matches_local(gpu):
     from pytorch_distributed_mnist_amd.data.mnist import synthetic_split
     from pytorch_distributed_mnist_amd.data.sampler import distributed_indices
     from pytorch_distributed_mnist_amd.parallel.comm import RcclComm
+    from pytorch_distributed_mnist_amd.runtime.gpu_step import GpuStepBase
     from pytorch_distributed_mnist_amd.runtime.program import build_local_program
-    train = synthetic_split(256 * 9 + 40, True)
+    train = synthetic_split(256 * (GpuStepBase.GRAPH_STEPS + 1) + 40, True)
     test = synthetic_split(256, False)
     out = []
     for force in (False, True):
@@ -76,8 +77,10 @@ def test_cnn_step_through_xgmi_matches_local(gpu):
 
 def _run_workers(nproc, tmp_path, **extra):
     # a peer that never arrives turns into an error after 10 s instead of a 60 s stall
+    # 8-step graphs: the workers' 9-step epochs replay two graphs (the carry crosses a replay
+    # boundary) in the step count the cross-transport tolerance below was set for
     env = dict(os.environ, PDM_SHARE_DEVICE="1", PDM_XGMI_OUT=str(tmp_path),
-               PDM_XGMI_TIMEOUT=os.environ.get("PDM_XGMI_TIMEOUT", "10"))
+               PDM_XGMI_TIMEOUT=os.environ.get("PDM_XGMI_TIMEOUT", "10"), PDM_GRAPH_STEPS="8")
     env.update(extra)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",

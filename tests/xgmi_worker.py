@@ -182,7 +182,7 @@ def train_model(arch, comm, dev, rank, ws, transport):
     opt = build_optimizer("sgd" if cnn else "adam", arena,
                           SimpleNamespace(lr=0.05 if cnn else 1e-3, momentum=0.9, weight_decay=1e-4))
     red = GradReducer(comm, arena.grads, spec.bucket_bounds(), transport=transport)
-    train = synthetic_split(128 * ws * 9 + 40, True)
+    train = synthetic_split(128 * ws * 9 + 40, True)   # 9 steps: graphs of 8 and 1 (the test sets 8)
     test = synthetic_split(256, False)
     prog = TrainProgram(arch, "bf16" if cnn else "fp32", arena, opt, red, train, test, 128,
                         use_graphs=True)
@@ -260,7 +260,7 @@ def absent_peer_streamed(comm, dev, rank, ws):
         prog.gpu.prepare(64)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        prog.gpu.train_steps(64, 2 * prog.gpu.GRAPH_STEPS + 3)     # graphs of 8, 8, 2, 1 steps
+        prog.gpu.train_steps(64, 2 * prog.gpu.GRAPH_STEPS + 3)     # two full graphs and one of 3 steps
         torch.cuda.synchronize()
         out["elapsed_s"] = time.perf_counter() - t0
         out["error"] = int(red._xgmi.native.error())
