@@ -49,7 +49,10 @@ def main():
     for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         print(f"| {k} | {len(v)} | {sum(v):.1f} | {statistics.mean(v):.2f} | {min(v):.2f} | "
               f"{max(v):.2f} | {100 * sum(v) / total:.1f} |")
-    step = {k: statistics.mean(v) for k, v in per.items() if len(v) >= a.steps}
+    # torch / runtime kernels (graph capture and upload fills, copies) are not step kernels,
+    # however often they run
+    step = {k: statistics.mean(v) for k, v in per.items()
+            if len(v) >= a.steps and not k.startswith(("at::", "__amd"))}
     if step:
         print(f"\nper-step kernels (called >= {a.steps}x): sum of means = "
               f"{sum(step.values()):.1f} us")
